@@ -1,0 +1,257 @@
+/*
+ * psg.h — C-ABI of the MI355X parameter-server value store and data path.
+ *
+ * This is the drop-in boundary between the C++ host runtime (the ps::KVWorker /
+ * ps::KVServer mirror under parameter-server_amd/ps/) and the HIP kernels for
+ * gfx950 in parameter-server_amd/csrc/.  Every entry point is plain C: raw
+ * pointers, sizes and an int status.  No exception crosses it, no torch type
+ * appears in it.  The detail of a failure is in psg_last_error() (per thread).
+ *
+ * Reference interfaces each group replaces (paths relative to the reference
+ * repository SovietPower/Parameter-Server):
+ *
+ *   psg_store_*      the server-side value store `std::unordered_map<Key,V> store`
+ *                    of KVServerDefaultHandle            src/ps/KVApp.h:433-458
+ *   psg_store_handle the per-request accumulate loop
+ *                    `store[key] += vals[i]; res.vals[i] = store[key]`
+ *                                                        src/ps/KVApp.h:446-454
+ *   psg_server_ranges PostOffice::GetServerRanges        src/internal/PostOffice.cpp:211-221
+ *   psg_slice        KVWorker<V>::DefaultSlicer           src/ps/KVApp.h:515-574
+ *   psg_merge        the AddPullCB merge lambda           src/ps/KVApp.h:673-726
+ *   psg_comm_*       the ZMQ data path of Van::Send / ZMQVan::SendMsg / ReceiveMsg
+ *                    (src/internal/Van.cpp:170-179, src/internal/ZMQVan.cpp:147-248)
+ *                    for the BSP case: Push = reduce-scatter + accumulate,
+ *                    Pull = all-gather, over RCCL / xGMI
+ *   psg_lr_apply     LRServer::RequestHandle sync-mode apply (SGD / Adam)
+ *                                                        tests/src/LRServer.h:151-189,
+ *                                                        tests/src/Adam.h:28-34
+ *
+ * Conventions
+ *   - All data pointers passed to compute entry points are DEVICE pointers
+ *     (hipMalloc'd, or psg_malloc'd) unless the parameter name ends in _host.
+ *   - Work is stream-ordered on the given stream (NULL = the legacy default
+ *     stream).  An entry point that must return a host value (psg_slice,
+ *     psg_store_resolve with insert) synchronises that stream itself and says so.
+ *   - The store owns its device memory.  Buffers passed in stay owned by the
+ *     caller and must stay valid until the stream has executed the work.
+ *   - One store per server shard; calls on one store must be serialised by the
+ *     caller (the reference runs ReqHandle on a single Customer thread,
+ *     src/internal/Customer.cpp:52-70).
+ */
+#ifndef PSG_H_
+#define PSG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSG_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+enum {
+  PSG_OK = 0,
+  PSG_ERR_INVALID = 1,     /* bad argument (a reference CHECK would have thrown) */
+  PSG_ERR_HIP = 2,         /* HIP runtime error */
+  PSG_ERR_OOM = 3,         /* device allocation failed */
+  PSG_ERR_RANGE = 4,       /* key outside the store's range / capacity */
+  PSG_ERR_COMM = 5,        /* RCCL error */
+  PSG_ERR_UNSUPPORTED = 6  /* dtype / kind combination not built */
+};
+
+/* ---- value types (Message.h DataType has no half; f16/bf16 are ours) --- */
+enum { PSG_F32 = 0, PSG_F64 = 1, PSG_F16 = 2, PSG_BF16 = 3 };
+
+/* ---- store kinds ------------------------------------------------------- */
+enum {
+  /* Slots cover keys [key_begin, key_begin + capacity) contiguously: key k lives
+   * at slot k - key_begin.  The layout of configs 2, 3 and 5 (dense vectors). */
+  PSG_STORE_DENSE = 0,
+  /* Arbitrary uint64 keys in [key_begin, key_end), kept as a sorted key array
+   * plus a value array in HBM.  A key is inserted on first touch with value 0,
+   * exactly like unordered_map::operator[] (KVApp.h:449, 452). */
+  PSG_STORE_SORTED = 1
+};
+
+/* ---- request flags (KVMeta::push / KVMeta::pull, KVApp.h:42-57) --------- */
+enum { PSG_PUSH = 1, PSG_PULL = 2 };
+
+typedef struct psg_store psg_store;
+typedef struct psg_comm psg_comm;
+typedef void* psg_stream; /* a hipStream_t */
+typedef void* psg_event;  /* a hipEvent_t */
+
+/* ======================================================================== */
+/* Runtime                                                                   */
+/* ======================================================================== */
+int psg_abi_version(void);
+/* Message of the last failed call on this thread ("" if none). */
+const char* psg_last_error(void);
+int psg_device_count(int* n);
+/* Bind the calling thread to a GPU (hipSetDevice). */
+int psg_set_device(int device);
+int psg_get_device(int* device);
+int psg_device_sync(void);
+
+int psg_malloc(void** dptr, size_t bytes);
+int psg_free(void* dptr);
+int psg_host_alloc(void** hptr, size_t bytes); /* pinned host memory */
+int psg_host_free(void* hptr);
+int psg_host_register(void* hptr, size_t bytes); /* pin a caller's heap range */
+int psg_host_unregister(void* hptr);
+/* kind: 0 = H2D, 1 = D2H, 2 = D2D, 3 = default (unified addressing) */
+int psg_memcpy(void* dst, const void* src, size_t bytes, int kind, psg_stream stream);
+int psg_memset(void* dptr, int value, size_t bytes, psg_stream stream);
+
+int psg_stream_create(psg_stream* stream);
+int psg_stream_destroy(psg_stream stream);
+int psg_stream_sync(psg_stream stream);
+int psg_event_create(psg_event* ev);
+int psg_event_destroy(psg_event ev);
+int psg_event_record(psg_event ev, psg_stream stream);
+int psg_event_sync(psg_event ev);
+int psg_event_elapsed_ms(psg_event start, psg_event stop, float* ms);
+
+/* Seeded synthetic data generated on the device: element i of the output is a
+ * pure function of (seed, i), so the CPU oracle regenerates it bit-exactly
+ * (oracle/ps_oracle.cpp: oracle_synth).
+ *   mode 0: integer-valued  floor(u * span) + lo        (exact float sums)
+ *   mode 1: real-valued     lo + u * (hi - lo)
+ * with u = (splitmix64(seed + i) >> 40) * 2^-24 in [0, 1). */
+int psg_fill_synth(void* dptr, uint64_t n, int dtype, uint64_t seed, int mode,
+                   double lo, double hi, psg_stream stream);
+/* keys[i] = base + i * step (the test_kv_app_benchmark key layout
+ * `kMaxKey / num * i + rank`, tests/test_kv_app_benchmark.cpp:47-52). */
+int psg_fill_keys_arith(uint64_t* keys, uint64_t n, uint64_t base, uint64_t step,
+                        psg_stream stream);
+
+/* ======================================================================== */
+/* Server-side value store  (KVServerDefaultHandle::store, KVApp.h:457)      */
+/* ======================================================================== */
+typedef struct psg_store_info {
+  int kind;
+  int dtype;
+  uint64_t key_begin;  /* owned key range [key_begin, key_end) */
+  uint64_t key_end;
+  uint64_t size;       /* keys currently present (dense: = capacity) */
+  uint64_t capacity;   /* slots allocated */
+  void* vals;          /* device pointer to the value array (slot order) */
+  uint64_t* keys;      /* device pointer to the sorted key array (SORTED), else NULL */
+} psg_store_info;
+
+int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end,
+                     uint64_t capacity, psg_store** out);
+int psg_store_destroy(psg_store* s);
+int psg_store_get_info(psg_store* s, psg_store_info* info);
+/* Zero every value (DENSE) / drop every key (SORTED). */
+int psg_store_clear(psg_store* s, psg_stream stream);
+
+/* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):
+ *   for i < n:  if (flags & PSG_PUSH) store[key_i] += vals[i];
+ *               if (flags & PSG_PULL) out[i] = store[key_i];   (post-update)
+ * keys == NULL means the consecutive keys first_key, first_key + 1, ...
+ * (dense request: no key array travels).  Keys must be strictly ascending
+ * (KVPairs contract, KVApp.h:23); a PULL of an absent key inserts it with 0.
+ * A DENSE store accepts only keys inside [key_begin, key_begin + capacity).
+ * vals/out are device arrays of n elements of the store's dtype. */
+int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,
+                     uint64_t first_key, const void* vals, void* out, uint64_t n,
+                     psg_stream stream);
+
+/* Slot cache (LR USE_KEY_CACHING, tests/src/LRServer.h:127-142): resolve a key
+ * list to slot indices once, then run requests by slot.  insert != 0 inserts
+ * absent keys (value 0) and synchronises the stream; insert == 0 writes
+ * UINT32_MAX for absent keys.  Slots stay valid until the next insert. */
+int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert,
+                      uint32_t* slots, psg_stream stream);
+int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots,
+                           const void* vals, void* out, uint64_t n,
+                           psg_stream stream);
+
+/* Copy the store to host memory (checkpoint, LRServer::SaveModel analogue,
+ * tests/src/LRServer.h:107-115).  keys_host may be NULL for a DENSE store;
+ * both arrays must hold info.size elements.  Synchronous. */
+int psg_store_dump(psg_store* s, uint64_t* keys_host, void* vals_host);
+
+/* ======================================================================== */
+/* Worker side: key-range slicing and pull merge                              */
+/* ======================================================================== */
+/* Server i owns [kMaxKey/ns*i, kMaxKey/ns*(i+1)), the last one ends at kMaxKey
+ * (PostOffice::GetServerRanges, PostOffice.cpp:211-221).  Host only. */
+int psg_server_ranges(int num_servers, uint64_t* begins_host, uint64_t* ends_host);
+
+/* DefaultSlicer (KVApp.h:515-574) on a device key array:
+ *   key_pos[0] = lower_bound(keys, begins[0]);
+ *   key_pos[i+1] = lower_bound(keys, ends[i])            (i < ns)
+ * and the value bounds of each slice:
+ *   lens == NULL:  val_pos[i] = key_pos[i] * (num_vals / n)   (CHECKs divisibility)
+ *   lens != NULL:  val_pos[i] = val_pos[0] + sum(lens[key_pos[0] .. key_pos[i]))
+ *                  (the running sum of KVApp.h:565-569; val_pos[0] = 0).
+ * key_pos_host / val_pos_host hold ns + 1 entries (val_pos_host may be NULL).
+ * Fails (PSG_ERR_INVALID) when key_pos[ns] != n, i.e. a key lies at or above
+ * the last range's end (the CHECK at KVApp.h:544).  Synchronises the stream. */
+int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_vals,
+              int num_servers, const uint64_t* begins_host,
+              const uint64_t* ends_host, uint64_t* key_pos_host,
+              uint64_t* val_pos_host, psg_stream stream);
+
+/* One pull reply (KVPairs from one server, KVApp.h:631-637). */
+typedef struct psg_segment {
+  const void* vals;    /* device pointer */
+  uint64_t count;      /* elements in vals */
+  uint64_t first_key;  /* keys.front() of the reply, the sort key */
+} psg_segment;
+
+/* The AddPullCB merge (KVApp.h:680-720): order the replies by first key and
+ * concatenate their values into dst (dst_count elements of elem_size bytes),
+ * in one batched-copy kernel.  Fails if the counts do not add up to dst_count
+ * (the "lost some servers?" CHECK, KVApp.h:691, 701). */
+int psg_merge(psg_segment* segs_host, int nsegs, int elem_size, void* dst,
+              uint64_t dst_count, psg_stream stream);
+
+/* ======================================================================== */
+/* Multi-GPU BSP data path over RCCL / xGMI (one server shard per GPU)        */
+/* ======================================================================== */
+/* Bytes of the opaque id rank 0 creates and every rank passes to init. */
+int psg_comm_id_bytes(void);
+int psg_comm_get_id(void* id_host);
+int psg_comm_init(const void* id_host, int nranks, int rank, psg_comm** out);
+int psg_comm_destroy(psg_comm* c);
+int psg_comm_rank(psg_comm* c, int* rank, int* nranks);
+
+/* BSP Push of a dense vector: every rank contributes its worker's full vector
+ * vals[n_total]; rank r's DENSE store `shard` owns the contiguous block
+ * [r * n_total / nranks, (r + 1) * n_total / nranks) (n_total % nranks == 0).
+ * shard += sum over ranks of vals[block r] — a reduce-scatter then the
+ * accumulate kernel.  `scratch` is a device buffer of n_total / nranks elements
+ * (NULL: the comm keeps one).  Equivalent to nranks KVWorker::Push calls
+ * arriving at each KVServerDefaultHandle (KVApp.h:449). */
+int psg_comm_push(psg_comm* c, psg_store* shard, const void* vals, uint64_t n_total,
+                  void* scratch, psg_stream stream);
+/* BSP Pull: out[n_total] on every rank = concatenation of every rank's shard,
+ * an all-gather (KVApp.h:452 + the merge of KVApp.h:713-720). */
+int psg_comm_pull(psg_comm* c, psg_store* shard, void* out, uint64_t n_total,
+                  psg_stream stream);
+
+/* ======================================================================== */
+/* LR server apply                                             */
+/* ======================================================================== */
+typedef struct psg_adam psg_adam;
+/* Adam state (m, v as double, Adam.h:14-18, 40-41) for n features. */
+int psg_adam_create(uint64_t n, double learning_rate, double beta1, double beta2,
+                    double epsilon, psg_adam** out);
+int psg_adam_destroy(psg_adam* a);
+/* weight[i] = (float)((double)weight[i] - g), with g = (double)(lr * merged[i])
+ * (an f32 product, as `double grad = learning_rate_ * merge_buf_.vals[i]`),
+ * then g = adam(g, i, iteration) when adam != NULL (LRServer.h:171-177,
+ * Adam.h:28-34); merged is f32, weights are the f32 DENSE store's slots
+ * [0, n).  Bit-identical to the reference's operation order. */
+int psg_lr_apply(psg_store* weights, const float* merged, uint64_t n, float lr,
+                 psg_adam* adam, int iteration, psg_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSG_H_ */

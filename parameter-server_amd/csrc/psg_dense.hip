@@ -1,0 +1,252 @@
+// psg_dense.hip — the element-wise accumulate kernels of the value store.
+//
+// Reference loop (src/ps/KVApp.h:446-454, KVServerDefaultHandle::operator()):
+//     for i < n:  if push: store[key_i] += vals[i];  if pull: res.vals[i] = store[key_i];
+// For a dense request the keys are consecutive, so key_i -> slot off + i and
+// the loop is a pure streaming op, bound by HBM:
+//     PUSH       read vals + read store + write store         12 B / f32 element
+//     PULL       read store + write out                         8 B / f32 element
+//     PUSH|PULL  read vals + read store + write store + write out 16 B / f32 element
+// No MFMA (0 flops of reuse).  Every lane moves 16 B per access (one
+// global_load_dwordx4, 1 KiB per wave instruction), each thread keeps U such
+// vectors of every stream in flight, blocks grid-stride over 256*U-vector
+// tiles (cdna_hip_programming.md Guidelines 11, 13, Appendix B 'Element-wise').
+// The once-read request stream (vals) and the write-only reply stream (out)
+// use non-temporal loads/stores; the store itself keeps the default policy so
+// a Pull that follows a Push can hit the Infinity Cache.
+#include <cstdlib>
+
+#include "psg_internal.h"
+
+namespace psg {
+
+template <int NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int NT>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// Vector kernel over nvec 16-byte vectors.  OP bits: PSG_PUSH, PSG_PULL.
+template <int DT, int OP, int U, int NT>
+__global__ __launch_bounds__(256) void k_dense_vec(u32x4* __restrict__ store,
+                                                   const u32x4* __restrict__ vals,
+                                                   u32x4* __restrict__ out, uint64_t nvec) {
+  using E = Elem<DT>;
+  const uint64_t tile = (uint64_t)kBlock * U;
+  const uint64_t gstride = (uint64_t)gridDim.x * tile;
+  for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += gstride) {
+    u32x4 s[U], v[U];
+    if (base + (uint64_t)(U - 1) * kBlock < nvec) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if constexpr ((OP & PSG_PUSH) != 0) v[u] = ld16<NT>(vals + i);
+        s[u] = ld16<0>(store + i);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if constexpr ((OP & PSG_PUSH) != 0) {
+          s[u] = E::add(s[u], v[u]);
+          st16<0>(store + i, s[u]);
+        }
+        if constexpr ((OP & PSG_PULL) != 0) st16<NT>(out + i, s[u]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) {
+          if constexpr ((OP & PSG_PUSH) != 0) v[u] = ld16<NT>(vals + i);
+          s[u] = ld16<0>(store + i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) {
+          if constexpr ((OP & PSG_PUSH) != 0) {
+            s[u] = E::add(s[u], v[u]);
+            st16<0>(store + i, s[u]);
+          }
+          if constexpr ((OP & PSG_PULL) != 0) st16<NT>(out + i, s[u]);
+        }
+      }
+    }
+  }
+}
+
+// Element kernel: misaligned operands and the sub-16-byte tail.
+template <int DT, int OP>
+__global__ __launch_bounds__(256) void k_dense_elem(typename Elem<DT>::T* __restrict__ store,
+                                                    const typename Elem<DT>::T* __restrict__ vals,
+                                                    typename Elem<DT>::T* __restrict__ out,
+                                                    uint64_t n) {
+  using E = Elem<DT>;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlock) {
+    typename E::T s = store[i];
+    if constexpr ((OP & PSG_PUSH) != 0) {
+      s = E::add1(s, vals[i]);
+      store[i] = s;
+    }
+    if constexpr ((OP & PSG_PULL) != 0) out[i] = s;
+  }
+}
+
+// Slot-indexed request: the gather/scatter form used by the SORTED store and
+// by cached slot lists.  UINT32_MAX slots are skipped (a pull yields 0).
+template <int DT, int OP>
+__global__ __launch_bounds__(256) void k_slots(typename Elem<DT>::T* __restrict__ store,
+                                               const uint32_t* __restrict__ slots,
+                                               const typename Elem<DT>::T* __restrict__ vals,
+                                               typename Elem<DT>::T* __restrict__ out, uint64_t n) {
+  using E = Elem<DT>;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t p = slots[i];
+    typename E::T s = (typename E::T)0.0f;
+    if (p != 0xffffffffu) {
+      s = store[p];
+      if constexpr ((OP & PSG_PUSH) != 0) {
+        s = E::add1(s, vals[i]);
+        store[p] = s;
+      }
+    }
+    if constexpr ((OP & PSG_PULL) != 0) out[i] = s;
+  }
+}
+
+// ---- tuning knobs (fixed defaults; env overrides exist for the sweep in
+// tools/sweep_dense.py only) ---------------------------------------------------
+struct DenseCfg {
+  int unroll = 4;
+  int nt = 1;
+  int blocks_per_cu = 8;
+};
+static DenseCfg dense_cfg() {
+  static DenseCfg cfg = [] {
+    DenseCfg c;
+    if (const char* e = getenv("PSG_DENSE_UNROLL")) c.unroll = atoi(e);
+    if (const char* e = getenv("PSG_DENSE_NT")) c.nt = atoi(e);
+    if (const char* e = getenv("PSG_DENSE_BPC")) c.blocks_per_cu = atoi(e);
+    if (c.unroll != 1 && c.unroll != 2 && c.unroll != 4 && c.unroll != 8) c.unroll = 4;
+    if (c.blocks_per_cu < 1 || c.blocks_per_cu > 32) c.blocks_per_cu = 8;
+    c.nt = c.nt ? 1 : 0;
+    return c;
+  }();
+  return cfg;
+}
+
+static unsigned stream_grid(uint64_t units, uint64_t per_block, int bpc) {
+  int cus = max_stream_blocks() / 8;
+  uint64_t cap = (uint64_t)cus * bpc;
+  uint64_t b = (units + per_block - 1) / per_block;
+  if (b > cap) b = cap;
+  if (b == 0) b = 1;
+  return (unsigned)b;
+}
+
+template <int DT, int OP, int U, int NT>
+static void launch_vec(void* store, const void* vals, void* out, uint64_t nvec, int bpc,
+                       hipStream_t s) {
+  unsigned g = stream_grid(nvec, (uint64_t)kBlock * U, bpc);
+  k_dense_vec<DT, OP, U, NT><<<g, kBlock, 0, s>>>((u32x4*)store, (const u32x4*)vals, (u32x4*)out,
+                                                  nvec);
+}
+
+template <int DT, int OP>
+static void dispatch_vec(const DenseCfg& c, void* store, const void* vals, void* out,
+                         uint64_t nvec, hipStream_t s) {
+#define PSG_V(U, NT)                                                      \
+  if (c.unroll == U && c.nt == NT) {                                      \
+    launch_vec<DT, OP, U, NT>(store, vals, out, nvec, c.blocks_per_cu, s); \
+    return;                                                               \
+  }
+  PSG_V(1, 0) PSG_V(1, 1) PSG_V(2, 0) PSG_V(2, 1) PSG_V(4, 0) PSG_V(4, 1) PSG_V(8, 0) PSG_V(8, 1)
+#undef PSG_V
+}
+
+template <int DT, int OP>
+static int run_dense(void* store, const void* vals, void* out, uint64_t n, hipStream_t s) {
+  using T = typename Elem<DT>::T;
+  constexpr int kVec = Elem<DT>::kVec;
+  const bool need_vals = (OP & PSG_PUSH) != 0, need_out = (OP & PSG_PULL) != 0;
+  bool vec_ok = aligned16(store) && (!need_vals || aligned16(vals)) && (!need_out || aligned16(out));
+  uint64_t nvec = vec_ok ? n / kVec : 0;
+  if (nvec) dispatch_vec<DT, OP>(dense_cfg(), store, vals, out, nvec, s);
+  uint64_t done = nvec * kVec;
+  if (done < n) {
+    uint64_t rest = n - done;
+    unsigned g = stream_grid(rest, kBlock, 8);
+    k_dense_elem<DT, OP><<<g, kBlock, 0, s>>>((T*)store + done,
+                                             need_vals ? (const T*)vals + done : nullptr,
+                                             need_out ? (T*)out + done : nullptr, rest);
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+template <int DT>
+static int run_dense_op(int op, void* store, const void* vals, void* out, uint64_t n,
+                        hipStream_t s) {
+  switch (op) {
+    case PSG_PUSH: return run_dense<DT, PSG_PUSH>(store, vals, out, n, s);
+    case PSG_PULL: return run_dense<DT, PSG_PULL>(store, vals, out, n, s);
+    case PSG_PUSH | PSG_PULL: return run_dense<DT, PSG_PUSH | PSG_PULL>(store, vals, out, n, s);
+    default: set_error("bad request flags %d", op); return PSG_ERR_INVALID;
+  }
+}
+
+int dense_request(int dtype, int op, void* store_vals, const void* vals, void* out, uint64_t n,
+                  hipStream_t stream) {
+  if (n == 0) return PSG_OK;
+  switch (dtype) {
+    case PSG_F32: return run_dense_op<PSG_F32>(op, store_vals, vals, out, n, stream);
+    case PSG_F64: return run_dense_op<PSG_F64>(op, store_vals, vals, out, n, stream);
+    case PSG_F16: return run_dense_op<PSG_F16>(op, store_vals, vals, out, n, stream);
+    case PSG_BF16: return run_dense_op<PSG_BF16>(op, store_vals, vals, out, n, stream);
+    default: set_error("unsupported dtype %d", dtype); return PSG_ERR_UNSUPPORTED;
+  }
+}
+
+template <int DT>
+static int run_slots(int op, void* store, const uint32_t* slots, const void* vals, void* out,
+                     uint64_t n, hipStream_t s) {
+  using T = typename Elem<DT>::T;
+  unsigned g = stream_grid(n, kBlock, 8);
+  switch (op) {
+    case PSG_PUSH:
+      k_slots<DT, PSG_PUSH><<<g, kBlock, 0, s>>>((T*)store, slots, (const T*)vals, (T*)out, n);
+      break;
+    case PSG_PULL:
+      k_slots<DT, PSG_PULL><<<g, kBlock, 0, s>>>((T*)store, slots, (const T*)vals, (T*)out, n);
+      break;
+    case PSG_PUSH | PSG_PULL:
+      k_slots<DT, PSG_PUSH | PSG_PULL><<<g, kBlock, 0, s>>>((T*)store, slots, (const T*)vals,
+                                                            (T*)out, n);
+      break;
+    default: set_error("bad request flags %d", op); return PSG_ERR_INVALID;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int slot_request(int dtype, int op, void* store_vals, const uint32_t* slots, const void* vals,
+                 void* out, uint64_t n, hipStream_t stream) {
+  if (n == 0) return PSG_OK;
+  switch (dtype) {
+    case PSG_F32: return run_slots<PSG_F32>(op, store_vals, slots, vals, out, n, stream);
+    case PSG_F64: return run_slots<PSG_F64>(op, store_vals, slots, vals, out, n, stream);
+    case PSG_F16: return run_slots<PSG_F16>(op, store_vals, slots, vals, out, n, stream);
+    case PSG_BF16: return run_slots<PSG_BF16>(op, store_vals, slots, vals, out, n, stream);
+    default: set_error("unsupported dtype %d", dtype); return PSG_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace psg

@@ -1,0 +1,152 @@
+// psg_internal.h — shared internals of the psg C-ABI implementation (gfx950).
+//
+// Error convention: every extern "C" entry returns an int status; the message
+// of the last failure is kept per thread (psg_last_error).  This replaces the
+// reference's CHECK -> ps_log::PSError throw (src/base/log.h:283-304), which
+// must not cross a C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/psg.h"
+
+namespace psg {
+
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void clear_error();
+
+// Status from a HIP call, with the message recorded.
+int hip_fail(hipError_t e, const char* what, const char* file, int line);
+
+}  // namespace psg
+
+#define PSG_HIP(call)                                                   \
+  do {                                                                  \
+    hipError_t e_ = (call);                                             \
+    if (e_ != hipSuccess) return psg::hip_fail(e_, #call, __FILE__, __LINE__); \
+  } while (0)
+
+#define PSG_REQUIRE(cond, code, ...)   \
+  do {                                 \
+    if (!(cond)) {                     \
+      psg::set_error(__VA_ARGS__);     \
+      return (code);                   \
+    }                                  \
+  } while (0)
+
+#define PSG_TRY(expr)             \
+  do {                            \
+    int rc_ = (expr);             \
+    if (rc_ != PSG_OK) return rc_; \
+  } while (0)
+
+namespace psg {
+
+// ---- element types --------------------------------------------------------
+inline int dtype_size(int dtype) {
+  switch (dtype) {
+    case PSG_F32: return 4;
+    case PSG_F64: return 8;
+    case PSG_F16: return 2;
+    case PSG_BF16: return 2;
+    default: return 0;
+  }
+}
+
+// 16-byte raw vector: the unit of every streaming load/store (one
+// global_load_dwordx4 per lane, 1 KiB per wave instruction).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// Per-dtype arithmetic on one 16-B vector.  Sub-32-bit types accumulate in
+// f32 and round once (RNE): with p(f32)=24 >= 2*p(f16)+2 the double rounding
+// is innocuous, so this equals exact-sum-rounded-to-half arithmetic.
+template <int DT> struct Elem;
+template <> struct Elem<PSG_F32> {
+  typedef float T;
+  static constexpr int kVec = 4;
+  __device__ static inline u32x4 add(u32x4 a, u32x4 b) {
+    f32x4 r = __builtin_bit_cast(f32x4, a) + __builtin_bit_cast(f32x4, b);
+    return __builtin_bit_cast(u32x4, r);
+  }
+  __device__ static inline T add1(T a, T b) { return a + b; }
+};
+template <> struct Elem<PSG_F64> {
+  typedef double T;
+  static constexpr int kVec = 2;
+  __device__ static inline u32x4 add(u32x4 a, u32x4 b) {
+    f64x2 r = __builtin_bit_cast(f64x2, a) + __builtin_bit_cast(f64x2, b);
+    return __builtin_bit_cast(u32x4, r);
+  }
+  __device__ static inline T add1(T a, T b) { return a + b; }
+};
+template <> struct Elem<PSG_F16> {
+  typedef _Float16 T;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f8 __attribute__((ext_vector_type(8)));
+  static constexpr int kVec = 8;
+  __device__ static inline u32x4 add(u32x4 a, u32x4 b) {
+    f8 fa = __builtin_convertvector(__builtin_bit_cast(h8, a), f8);
+    f8 fb = __builtin_convertvector(__builtin_bit_cast(h8, b), f8);
+    h8 r = __builtin_convertvector(fa + fb, h8);
+    return __builtin_bit_cast(u32x4, r);
+  }
+  __device__ static inline T add1(T a, T b) { return (T)((float)a + (float)b); }
+};
+template <> struct Elem<PSG_BF16> {
+  typedef __bf16 T;
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  typedef float f8 __attribute__((ext_vector_type(8)));
+  static constexpr int kVec = 8;
+  __device__ static inline u32x4 add(u32x4 a, u32x4 b) {
+    f8 fa = __builtin_convertvector(__builtin_bit_cast(b8, a), f8);
+    f8 fb = __builtin_convertvector(__builtin_bit_cast(b8, b), f8);
+    b8 r = __builtin_convertvector(fa + fb, b8);
+    return __builtin_bit_cast(u32x4, r);
+  }
+  __device__ static inline T add1(T a, T b) { return (T)((float)a + (float)b); }
+};
+
+// ---- launch geometry --------------------------------------------------------
+// Streaming kernels: 256-thread blocks, grid capped at 256 CUs x 8 blocks and
+// grid-strided beyond (cdna_hip_programming.md Guideline 11).
+constexpr int kBlock = 256;
+int max_stream_blocks();
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ---- store ------------------------------------------------------------------
+}  // namespace psg
+
+struct psg_store {
+  int kind;
+  int dtype;
+  int esize;
+  int device;
+  uint64_t key_begin, key_end;
+  uint64_t size;      // keys present
+  uint64_t capacity;  // slots allocated
+  void* vals;         // device, capacity * esize
+  uint64_t* keys;     // device, SORTED only
+  // scratch for SORTED requests (grown on demand)
+  uint32_t* slots;
+  uint64_t slots_cap;
+  int* flags;        // device int[4]: missing count, contiguous flag, ...
+  int* flags_host;   // pinned mirror
+};
+
+namespace psg {
+// Dense element-wise request on slot range [off, off + n) of a store value
+// array.  op = PSG_PUSH | PSG_PULL bits.  Implemented in psg_dense.hip.
+int dense_request(int dtype, int op, void* store_vals, const void* vals, void* out,
+                  uint64_t n, hipStream_t stream);
+// Slot-indexed request (gather/scatter).  psg_dense.hip.
+int slot_request(int dtype, int op, void* store_vals, const uint32_t* slots,
+                 const void* vals, void* out, uint64_t n, hipStream_t stream);
+}  // namespace psg

@@ -1,0 +1,227 @@
+// psg_runtime.hip — runtime entry points of the psg C-ABI: errors, device,
+// memory, streams, events, seeded synthetic data.
+#include <cstring>
+#include <mutex>
+
+#include "psg_internal.h"
+
+namespace psg {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+void clear_error() { g_err.clear(); }
+
+int hip_fail(hipError_t e, const char* what, const char* file, int line) {
+  set_error("%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+  return e == hipErrorOutOfMemory ? PSG_ERR_OOM : PSG_ERR_HIP;
+}
+
+int max_stream_blocks() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    cached[dev] = cus * 8;
+  }
+  return cached[dev];
+}
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_synth(T* __restrict__ out, uint64_t n, uint64_t seed,
+                                               int mode, double lo, double hi) {
+  const double inv24 = 1.0 / 16777216.0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t r = splitmix64(seed + i) >> 40;  // 24 random bits
+    double v;
+    if (mode == 0) {
+      v = floor((double)r * (hi - lo) * inv24) + lo;
+    } else {
+      v = lo + ((double)r * inv24) * (hi - lo);
+    }
+    // f16 / bf16 go through f32 (two RNE steps), restated exactly by the oracle.
+    if constexpr (sizeof(T) < 4) out[i] = (T)(float)v; else out[i] = (T)v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_keys_arith(uint64_t* __restrict__ keys, uint64_t n,
+                                                    uint64_t base, uint64_t step) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    keys[i] = base + i * step;
+}
+
+static unsigned grid_for(uint64_t n) {
+  uint64_t b = (n + kBlock - 1) / kBlock;
+  uint64_t cap = (uint64_t)max_stream_blocks();
+  if (b > cap) b = cap;
+  if (b == 0) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace psg
+
+using namespace psg;
+
+extern "C" {
+
+int psg_abi_version(void) { return PSG_ABI_VERSION; }
+const char* psg_last_error(void) { return g_err.c_str(); }
+
+int psg_device_count(int* n) {
+  PSG_REQUIRE(n, PSG_ERR_INVALID, "psg_device_count: null out");
+  PSG_HIP(hipGetDeviceCount(n));
+  return PSG_OK;
+}
+int psg_set_device(int device) {
+  PSG_HIP(hipSetDevice(device));
+  return PSG_OK;
+}
+int psg_get_device(int* device) {
+  PSG_REQUIRE(device, PSG_ERR_INVALID, "psg_get_device: null out");
+  PSG_HIP(hipGetDevice(device));
+  return PSG_OK;
+}
+int psg_device_sync(void) {
+  PSG_HIP(hipDeviceSynchronize());
+  return PSG_OK;
+}
+
+int psg_malloc(void** dptr, size_t bytes) {
+  PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_malloc: null out");
+  *dptr = nullptr;
+  if (bytes == 0) return PSG_OK;
+  PSG_HIP(hipMalloc(dptr, bytes));
+  return PSG_OK;
+}
+int psg_free(void* dptr) {
+  if (dptr) PSG_HIP(hipFree(dptr));
+  return PSG_OK;
+}
+int psg_host_alloc(void** hptr, size_t bytes) {
+  PSG_REQUIRE(hptr, PSG_ERR_INVALID, "psg_host_alloc: null out");
+  *hptr = nullptr;
+  if (bytes == 0) return PSG_OK;
+  PSG_HIP(hipHostMalloc(hptr, bytes, hipHostMallocDefault));
+  return PSG_OK;
+}
+int psg_host_free(void* hptr) {
+  if (hptr) PSG_HIP(hipHostFree(hptr));
+  return PSG_OK;
+}
+int psg_host_register(void* hptr, size_t bytes) {
+  PSG_REQUIRE(hptr && bytes, PSG_ERR_INVALID, "psg_host_register: empty range");
+  PSG_HIP(hipHostRegister(hptr, bytes, hipHostRegisterDefault));
+  return PSG_OK;
+}
+int psg_host_unregister(void* hptr) {
+  PSG_HIP(hipHostUnregister(hptr));
+  return PSG_OK;
+}
+
+int psg_memcpy(void* dst, const void* src, size_t bytes, int kind, psg_stream stream) {
+  if (bytes == 0) return PSG_OK;
+  PSG_REQUIRE(dst && src, PSG_ERR_INVALID, "psg_memcpy: null pointer");
+  hipMemcpyKind k;
+  switch (kind) {
+    case 0: k = hipMemcpyHostToDevice; break;
+    case 1: k = hipMemcpyDeviceToHost; break;
+    case 2: k = hipMemcpyDeviceToDevice; break;
+    case 3: k = hipMemcpyDefault; break;
+    default: set_error("psg_memcpy: bad kind %d", kind); return PSG_ERR_INVALID;
+  }
+  PSG_HIP(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
+  return PSG_OK;
+}
+int psg_memset(void* dptr, int value, size_t bytes, psg_stream stream) {
+  if (bytes == 0) return PSG_OK;
+  PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_memset: null pointer");
+  PSG_HIP(hipMemsetAsync(dptr, value, bytes, (hipStream_t)stream));
+  return PSG_OK;
+}
+
+int psg_stream_create(psg_stream* stream) {
+  PSG_REQUIRE(stream, PSG_ERR_INVALID, "psg_stream_create: null out");
+  hipStream_t s;
+  PSG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = (psg_stream)s;
+  return PSG_OK;
+}
+int psg_stream_destroy(psg_stream stream) {
+  if (stream) PSG_HIP(hipStreamDestroy((hipStream_t)stream));
+  return PSG_OK;
+}
+int psg_stream_sync(psg_stream stream) {
+  PSG_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return PSG_OK;
+}
+int psg_event_create(psg_event* ev) {
+  PSG_REQUIRE(ev, PSG_ERR_INVALID, "psg_event_create: null out");
+  hipEvent_t e;
+  PSG_HIP(hipEventCreate(&e));
+  *ev = (psg_event)e;
+  return PSG_OK;
+}
+int psg_event_destroy(psg_event ev) {
+  if (ev) PSG_HIP(hipEventDestroy((hipEvent_t)ev));
+  return PSG_OK;
+}
+int psg_event_record(psg_event ev, psg_stream stream) {
+  PSG_HIP(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+  return PSG_OK;
+}
+int psg_event_sync(psg_event ev) {
+  PSG_HIP(hipEventSynchronize((hipEvent_t)ev));
+  return PSG_OK;
+}
+int psg_event_elapsed_ms(psg_event start, psg_event stop, float* ms) {
+  PSG_REQUIRE(ms, PSG_ERR_INVALID, "psg_event_elapsed_ms: null out");
+  PSG_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+  return PSG_OK;
+}
+
+int psg_fill_synth(void* dptr, uint64_t n, int dtype, uint64_t seed, int mode, double lo,
+                   double hi, psg_stream stream) {
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_fill_synth: null pointer");
+  PSG_REQUIRE(mode == 0 || mode == 1, PSG_ERR_INVALID, "psg_fill_synth: bad mode %d", mode);
+  hipStream_t s = (hipStream_t)stream;
+  unsigned g = grid_for(n);
+  switch (dtype) {
+    case PSG_F32: k_synth<float><<<g, kBlock, 0, s>>>((float*)dptr, n, seed, mode, lo, hi); break;
+    case PSG_F64: k_synth<double><<<g, kBlock, 0, s>>>((double*)dptr, n, seed, mode, lo, hi); break;
+    case PSG_F16: k_synth<_Float16><<<g, kBlock, 0, s>>>((_Float16*)dptr, n, seed, mode, lo, hi); break;
+    case PSG_BF16: k_synth<__bf16><<<g, kBlock, 0, s>>>((__bf16*)dptr, n, seed, mode, lo, hi); break;
+    default: set_error("psg_fill_synth: bad dtype %d", dtype); return PSG_ERR_UNSUPPORTED;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int psg_fill_keys_arith(uint64_t* keys, uint64_t n, uint64_t base, uint64_t step,
+                        psg_stream stream) {
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(keys, PSG_ERR_INVALID, "psg_fill_keys_arith: null pointer");
+  k_keys_arith<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(keys, n, base, step);
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+}  // extern "C"

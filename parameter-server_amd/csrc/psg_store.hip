@@ -1,0 +1,557 @@
+// psg_store.hip — the server-side value store in HBM and the request handle.
+//
+// Replaces `std::unordered_map<Key, Value> store` of KVServerDefaultHandle
+// (src/ps/KVApp.h:433-458).  Two layouts:
+//
+//   DENSE   one value array; key k at slot k - key_begin.  A request with
+//           consecutive keys (keys == NULL) is one streaming kernel
+//           (psg_dense.hip).
+//   SORTED  a sorted uint64 key array K[0..size) and a value array V in the
+//           same order.  A request (sorted, unique keys — the KVPairs contract,
+//           KVApp.h:23) is resolved to slots by a block-narrowed lower_bound:
+//           each block takes a 1024-key tile, finds the window of K its first
+//           and last key bracket, and every lane binary-searches inside that
+//           window (L2-resident when the request is dense in K).  When the
+//           resolved slots are one contiguous run (the steady state of a worker
+//           that pushes the same key set, test_kv_app*.cpp, LR_ps) the request
+//           runs as the dense streaming kernel on V + slot0.  Keys that are
+//           absent are inserted with value 0 before the request is applied —
+//           the `operator[]` insert of KVApp.h:449/452 — by a parallel merge of
+//           the (compacted, sorted) new keys into K and V.
+#include <algorithm>
+#include <cstring>
+
+#include "psg_internal.h"
+
+namespace psg {
+
+constexpr int kTile = 1024;  // request keys per block tile (4 per lane)
+constexpr uint32_t kNoSlot = 0xffffffffu;
+
+enum { F_MISSING = 0, F_NONCONTIG = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
+
+__device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__ a, uint64_t lo,
+                                                    uint64_t hi, uint64_t key) {
+  while (lo < hi) {
+    uint64_t mid = lo + ((hi - lo) >> 1);
+    if (a[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Resolve sorted request keys q[0..n) against K[0..S).  slots[i] = index of
+// q[i] in K, or kNoSlot.  flags: [F_MISSING] += absent keys, [F_NONCONTIG] |=
+// slots not equal to base + i, [F_RANGE] |= key outside [kb, ke),
+// [F_UNSORTED] |= q not strictly ascending.
+__global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q, uint64_t n,
+                                                 const uint64_t* __restrict__ K, uint64_t S,
+                                                 uint64_t kb, uint64_t ke,
+                                                 uint32_t* __restrict__ slots,
+                                                 int* __restrict__ flags) {
+  __shared__ uint64_t win[3];
+  int missing = 0, noncontig = 0, range = 0, unsorted = 0;
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * kTile;
+    const uint64_t t1 = (t0 + kTile < n) ? t0 + kTile : n;
+    if (threadIdx.x == 0) win[0] = lower_bound_dev(K, 0, S, q[t0]);
+    if (threadIdx.x == 64) {
+      uint64_t hi = lower_bound_dev(K, 0, S, q[t1 - 1]);
+      win[1] = hi < S ? hi + 1 : S;
+    }
+    if (threadIdx.x == 128) win[2] = lower_bound_dev(K, 0, S, q[0]);
+    __syncthreads();
+    const uint64_t lo = win[0], hi = win[1], base = win[2];
+    for (uint64_t i = t0 + threadIdx.x; i < t1; i += kBlock) {
+      const uint64_t key = q[i];
+      if (key < kb || key >= ke) range = 1;
+      if (i > 0 && q[i - 1] >= key) unsorted = 1;
+      const uint64_t p = lower_bound_dev(K, lo, hi, key);
+      const bool found = p < S && K[p] == key;
+      slots[i] = found ? (uint32_t)p : kNoSlot;
+      if (!found) missing++;
+      if (!found || p != base + i) noncontig = 1;
+    }
+    __syncthreads();
+  }
+  // one atomic per wave per flag (the compiler aggregates uniform adds)
+  if (missing) atomicAdd(&flags[F_MISSING], missing);
+  if (noncontig) atomicOr(&flags[F_NONCONTIG], 1);
+  if (range) atomicOr(&flags[F_RANGE], 1);
+  if (unsorted) atomicOr(&flags[F_UNSORTED], 1);
+}
+
+// Block-wide exclusive scan helper over 256 lanes (wave = 64).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t wsum[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < w) off += wsum[k];
+    tot += wsum[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return off + x - v;
+}
+
+// Pass 1 of the compaction: absent-key count per 1024-key tile.
+__global__ __launch_bounds__(256) void k_tile_missing(const uint32_t* __restrict__ slots, uint64_t n,
+                                                      uint32_t* __restrict__ counts) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    uint64_t i = t0 + (uint64_t)k * kBlock + threadIdx.x;
+    if (i < n && slots[i] == kNoSlot) c++;
+  }
+  uint32_t tot;
+  block_excl_scan(c, &tot);
+  if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+
+// Exclusive scan of the per-tile counts, single block (ntiles is small:
+// n / 1024).
+__global__ __launch_bounds__(256) void k_scan_counts(uint32_t* __restrict__ counts, uint64_t ntiles) {
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t b = 0; b < ntiles; b += kBlock) {
+    uint64_t i = b + threadIdx.x;
+    uint32_t v = i < ntiles ? counts[i] : 0;
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(v, &tot);
+    if (i < ntiles) counts[i] = carry + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+}
+
+// Pass 2: write the absent keys, in order, to miss[].
+__global__ __launch_bounds__(256) void k_compact_missing(const uint64_t* __restrict__ q,
+                                                         const uint32_t* __restrict__ slots,
+                                                         uint64_t n,
+                                                         const uint32_t* __restrict__ offs,
+                                                         uint64_t* __restrict__ miss) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  // each lane owns 4 consecutive keys so the order inside the tile is kept
+  const uint64_t i0 = t0 + (uint64_t)threadIdx.x * (kTile / kBlock);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    uint64_t i = i0 + k;
+    if (i < n && slots[i] == kNoSlot) c++;
+  }
+  uint32_t tot;
+  uint32_t pos = offs[blockIdx.x] + block_excl_scan(c, &tot);
+#pragma unroll
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    uint64_t i = i0 + k;
+    if (i < n && slots[i] == kNoSlot) miss[pos++] = q[i];
+  }
+}
+
+// Merge: old element j goes to j + #(new keys < K[j]); new key t goes to
+// t + #(old keys < M[t]).
+template <typename T>
+__global__ __launch_bounds__(256) void k_merge_old(const uint64_t* __restrict__ K,
+                                                   const T* __restrict__ V, uint64_t S,
+                                                   const uint64_t* __restrict__ M, uint64_t m,
+                                                   uint64_t* __restrict__ K2, T* __restrict__ V2) {
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < S;
+       j += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t key = K[j];
+    const uint64_t d = j + lower_bound_dev(M, 0, m, key);
+    K2[d] = key;
+    V2[d] = V[j];
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_merge_new(const uint64_t* __restrict__ K, uint64_t S,
+                                                   const uint64_t* __restrict__ M, uint64_t m,
+                                                   uint64_t* __restrict__ K2, T* __restrict__ V2) {
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < m;
+       t += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t key = M[t];
+    const uint64_t d = t + lower_bound_dev(K, 0, S, key);
+    K2[d] = key;
+    V2[d] = (T)0.0f;
+  }
+}
+
+// DENSE store addressed by explicit keys: slot = key - key_begin.
+template <int DT, int OP>
+__global__ __launch_bounds__(256) void k_dense_keyed(typename Elem<DT>::T* __restrict__ store,
+                                                     uint64_t kb, uint64_t cap,
+                                                     const uint64_t* __restrict__ keys,
+                                                     const typename Elem<DT>::T* __restrict__ vals,
+                                                     typename Elem<DT>::T* __restrict__ out,
+                                                     uint64_t n, int* __restrict__ flags) {
+  using E = Elem<DT>;
+  int bad = 0, unsorted = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t key = keys[i];
+    if (i > 0 && keys[i - 1] >= key) unsorted = 1;
+    const uint64_t p = key - kb;  // wraps for key < kb
+    if (key < kb || p >= cap) {
+      bad = 1;
+      continue;
+    }
+    typename E::T s = store[p];
+    if constexpr ((OP & PSG_PUSH) != 0) {
+      s = E::add1(s, vals[i]);
+      store[p] = s;
+    }
+    if constexpr ((OP & PSG_PULL) != 0) out[i] = s;
+  }
+  if (bad) atomicOr(&flags[F_RANGE], 1);
+  if (unsorted) atomicOr(&flags[F_UNSORTED], 1);
+}
+
+// Slots of a DENSE store: key - key_begin (kNoSlot when outside).
+__global__ __launch_bounds__(256) void k_dense_slots(const uint64_t* __restrict__ keys, uint64_t n,
+                                                     uint64_t kb, uint64_t cap,
+                                                     uint32_t* __restrict__ slots,
+                                                     int* __restrict__ flags) {
+  int bad = 0, unsorted = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t key = keys[i];
+    if (i > 0 && keys[i - 1] >= key) unsorted = 1;
+    const uint64_t p = key - kb;
+    const bool ok = key >= kb && p < cap && p < 0xffffffffull;
+    if (!ok) bad = 1;
+    slots[i] = ok ? (uint32_t)p : kNoSlot;
+  }
+  if (bad) atomicOr(&flags[F_RANGE], 1);
+  if (unsorted) atomicOr(&flags[F_UNSORTED], 1);
+}
+
+static unsigned grid_n(uint64_t n, uint64_t per_block) {
+  uint64_t b = (n + per_block - 1) / per_block;
+  uint64_t cap = (uint64_t)max_stream_blocks();
+  if (b > cap) b = cap;
+  return b ? (unsigned)b : 1u;
+}
+
+static int ensure_slots(psg_store* s, uint64_t n) {
+  if (s->slots_cap >= n) return PSG_OK;
+  if (s->slots) PSG_HIP(hipFree(s->slots));
+  s->slots = nullptr;
+  uint64_t cap = std::max<uint64_t>(n, 1 << 16);
+  PSG_HIP(hipMalloc(&s->slots, cap * sizeof(uint32_t)));
+  s->slots_cap = cap;
+  return PSG_OK;
+}
+
+static int read_flags(psg_store* s, hipStream_t st) {
+  PSG_HIP(hipMemcpyAsync(s->flags_host, s->flags, F_NFLAGS * sizeof(int), hipMemcpyDeviceToHost, st));
+  PSG_HIP(hipStreamSynchronize(st));
+  return PSG_OK;
+}
+
+template <typename T>
+static int merge_insert(psg_store* s, const uint64_t* miss, uint64_t m, hipStream_t st) {
+  const uint64_t S = s->size;
+  uint64_t cap = s->capacity;
+  if (S + m > cap) {
+    cap = std::max<uint64_t>(S + m, cap * 2);
+    cap = std::max<uint64_t>(cap, 1024);
+  }
+  PSG_REQUIRE(cap <= 0xfffffffeull, PSG_ERR_RANGE, "SORTED store: more than 2^32-2 keys");
+  uint64_t* K2 = nullptr;
+  T* V2 = nullptr;
+  PSG_HIP(hipMalloc((void**)&K2, cap * sizeof(uint64_t)));
+  PSG_HIP(hipMalloc((void**)&V2, cap * sizeof(T)));
+  if (S) k_merge_old<T><<<grid_n(S, kBlock), kBlock, 0, st>>>(s->keys, (const T*)s->vals, S, miss, m, K2, V2);
+  k_merge_new<T><<<grid_n(m, kBlock), kBlock, 0, st>>>(s->keys, S, miss, m, K2, V2);
+  PSG_HIP(hipGetLastError());
+  PSG_HIP(hipStreamSynchronize(st));
+  if (s->keys) PSG_HIP(hipFree(s->keys));
+  if (s->vals) PSG_HIP(hipFree(s->vals));
+  s->keys = K2;
+  s->vals = V2;
+  s->size = S + m;
+  s->capacity = cap;
+  return PSG_OK;
+}
+
+static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, uint64_t m, hipStream_t st) {
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  uint32_t* counts = nullptr;
+  uint64_t* miss = nullptr;
+  PSG_HIP(hipMalloc((void**)&counts, ntiles * sizeof(uint32_t)));
+  PSG_HIP(hipMalloc((void**)&miss, m * sizeof(uint64_t)));
+  k_tile_missing<<<(unsigned)ntiles, kBlock, 0, st>>>(s->slots, n, counts);
+  k_scan_counts<<<1, kBlock, 0, st>>>(counts, ntiles);
+  k_compact_missing<<<(unsigned)ntiles, kBlock, 0, st>>>(q, s->slots, n, counts, miss);
+  PSG_HIP(hipGetLastError());
+  int rc;
+  switch (s->dtype) {
+    case PSG_F32: rc = merge_insert<float>(s, miss, m, st); break;
+    case PSG_F64: rc = merge_insert<double>(s, miss, m, st); break;
+    case PSG_F16: rc = merge_insert<_Float16>(s, miss, m, st); break;
+    case PSG_BF16: rc = merge_insert<__bf16>(s, miss, m, st); break;
+    default: rc = PSG_ERR_UNSUPPORTED;
+  }
+  PSG_HIP(hipStreamSynchronize(st));
+  PSG_HIP(hipFree(counts));
+  PSG_HIP(hipFree(miss));
+  return rc;
+}
+
+// Resolve q against the SORTED store, inserting absent keys when asked.
+// On return s->slots[0..n) holds the slots; *contig_base = slot of q[0] when
+// the slots are one contiguous run (else UINT64_MAX).
+static int sorted_resolve(psg_store* s, const uint64_t* q, uint64_t n, bool insert,
+                          uint64_t* contig_base, hipStream_t st) {
+  PSG_TRY(ensure_slots(s, n));
+  for (int pass = 0; pass < 2; ++pass) {
+    PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+    const uint64_t ntiles = (n + kTile - 1) / kTile;
+    k_resolve<<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size, s->key_begin,
+                                                    s->key_end, s->slots, s->flags);
+    PSG_HIP(hipGetLastError());
+    PSG_TRY(read_flags(s, st));
+    const int* f = s->flags_host;
+    PSG_REQUIRE(!f[F_UNSORTED], PSG_ERR_INVALID,
+                "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
+    PSG_REQUIRE(!f[F_RANGE], PSG_ERR_RANGE, "request key outside the store range [%llu, %llu)",
+                (unsigned long long)s->key_begin, (unsigned long long)s->key_end);
+    if (f[F_MISSING] == 0 || !insert) {
+      if (contig_base) {
+        *contig_base = UINT64_MAX;
+        if (!f[F_NONCONTIG] && f[F_MISSING] == 0) {
+          uint32_t p0;
+          PSG_HIP(hipMemcpyAsync(&p0, s->slots, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+          PSG_HIP(hipStreamSynchronize(st));
+          *contig_base = p0;
+        }
+      }
+      return PSG_OK;
+    }
+    PSG_REQUIRE(pass == 0, PSG_ERR_HIP, "SORTED store: keys still absent after insert");
+    PSG_TRY(insert_missing(s, q, n, (uint64_t)f[F_MISSING], st));
+  }
+  return PSG_OK;
+}
+
+template <int DT>
+static int run_dense_keyed(psg_store* s, int op, const uint64_t* keys, const void* vals, void* out,
+                           uint64_t n, hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  unsigned g = grid_n(n, kBlock);
+  switch (op) {
+    case PSG_PUSH:
+      k_dense_keyed<DT, PSG_PUSH><<<g, kBlock, 0, st>>>((T*)s->vals, s->key_begin, s->capacity, keys,
+                                                        (const T*)vals, (T*)out, n, s->flags);
+      break;
+    case PSG_PULL:
+      k_dense_keyed<DT, PSG_PULL><<<g, kBlock, 0, st>>>((T*)s->vals, s->key_begin, s->capacity, keys,
+                                                        (const T*)vals, (T*)out, n, s->flags);
+      break;
+    default:
+      k_dense_keyed<DT, PSG_PUSH | PSG_PULL><<<g, kBlock, 0, st>>>(
+          (T*)s->vals, s->key_begin, s->capacity, keys, (const T*)vals, (T*)out, n, s->flags);
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+}  // namespace psg
+
+using namespace psg;
+
+extern "C" {
+
+int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, uint64_t capacity,
+                     psg_store** out) {
+  PSG_REQUIRE(out, PSG_ERR_INVALID, "psg_store_create: null out");
+  *out = nullptr;
+  PSG_REQUIRE(kind == PSG_STORE_DENSE || kind == PSG_STORE_SORTED, PSG_ERR_INVALID,
+              "psg_store_create: bad kind %d", kind);
+  const int es = dtype_size(dtype);
+  PSG_REQUIRE(es > 0, PSG_ERR_UNSUPPORTED, "psg_store_create: bad dtype %d", dtype);
+  PSG_REQUIRE(key_begin < key_end, PSG_ERR_INVALID, "psg_store_create: empty key range");
+  if (kind == PSG_STORE_DENSE)
+    PSG_REQUIRE(capacity > 0 && capacity <= key_end - key_begin, PSG_ERR_INVALID,
+                "psg_store_create: DENSE capacity %llu does not fit the key range",
+                (unsigned long long)capacity);
+  psg_store* s = new psg_store();
+  memset(s, 0, sizeof(*s));
+  s->kind = kind;
+  s->dtype = dtype;
+  s->esize = es;
+  s->key_begin = key_begin;
+  s->key_end = key_end;
+  (void)hipGetDevice(&s->device);
+  auto fail = [&](int rc) {
+    psg_store_destroy(s);
+    return rc;
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&s->flags, F_NFLAGS * sizeof(int))) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(flags)", __FILE__, __LINE__));
+  if ((e = hipHostMalloc(&s->flags_host, F_NFLAGS * sizeof(int), hipHostMallocDefault)) != hipSuccess)
+    return fail(hip_fail(e, "hipHostMalloc(flags)", __FILE__, __LINE__));
+  if (kind == PSG_STORE_DENSE) {
+    s->capacity = capacity;
+    s->size = capacity;
+    if ((e = hipMalloc(&s->vals, capacity * es)) != hipSuccess)
+      return fail(hip_fail(e, "hipMalloc(store values)", __FILE__, __LINE__));
+    if ((e = hipMemset(s->vals, 0, capacity * es)) != hipSuccess)
+      return fail(hip_fail(e, "hipMemset(store values)", __FILE__, __LINE__));
+  } else {
+    s->capacity = 0;
+    s->size = 0;
+    if (capacity > 0) {
+      PSG_REQUIRE(capacity <= 0xfffffffeull, PSG_ERR_RANGE, "SORTED store capacity above 2^32-2");
+      if ((e = hipMalloc(&s->vals, capacity * es)) != hipSuccess)
+        return fail(hip_fail(e, "hipMalloc(store values)", __FILE__, __LINE__));
+      if ((e = hipMalloc(&s->keys, capacity * sizeof(uint64_t))) != hipSuccess)
+        return fail(hip_fail(e, "hipMalloc(store keys)", __FILE__, __LINE__));
+      s->capacity = capacity;
+    }
+  }
+  *out = s;
+  return PSG_OK;
+}
+
+int psg_store_destroy(psg_store* s) {
+  if (!s) return PSG_OK;
+  if (s->vals) (void)hipFree(s->vals);
+  if (s->keys) (void)hipFree(s->keys);
+  if (s->slots) (void)hipFree(s->slots);
+  if (s->flags) (void)hipFree(s->flags);
+  if (s->flags_host) (void)hipHostFree(s->flags_host);
+  delete s;
+  return PSG_OK;
+}
+
+int psg_store_get_info(psg_store* s, psg_store_info* info) {
+  PSG_REQUIRE(s && info, PSG_ERR_INVALID, "psg_store_get_info: null argument");
+  info->kind = s->kind;
+  info->dtype = s->dtype;
+  info->key_begin = s->key_begin;
+  info->key_end = s->key_end;
+  info->size = s->size;
+  info->capacity = s->capacity;
+  info->vals = s->vals;
+  info->keys = s->keys;
+  return PSG_OK;
+}
+
+int psg_store_clear(psg_store* s, psg_stream stream) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_clear: null store");
+  if (s->kind == PSG_STORE_DENSE) {
+    PSG_HIP(hipMemsetAsync(s->vals, 0, s->capacity * s->esize, (hipStream_t)stream));
+  } else {
+    s->size = 0;
+  }
+  return PSG_OK;
+}
+
+int psg_store_handle(psg_store* s, int flags, const uint64_t* keys, uint64_t first_key,
+                     const void* vals, void* out, uint64_t n, psg_stream stream) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_handle: null store");
+  PSG_REQUIRE(flags >= 1 && flags <= 3, PSG_ERR_INVALID, "psg_store_handle: bad flags %d", flags);
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(!(flags & PSG_PUSH) || vals, PSG_ERR_INVALID, "push without vals");
+  PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
+  hipStream_t st = (hipStream_t)stream;
+  if (s->kind == PSG_STORE_DENSE) {
+    if (!keys) {
+      PSG_REQUIRE(first_key >= s->key_begin && first_key - s->key_begin <= s->capacity &&
+                      n <= s->capacity - (first_key - s->key_begin),
+                  PSG_ERR_RANGE, "dense request [%llu, +%llu) outside store slots [%llu, +%llu)",
+                  (unsigned long long)first_key, (unsigned long long)n,
+                  (unsigned long long)s->key_begin, (unsigned long long)s->capacity);
+      char* base = (char*)s->vals + (first_key - s->key_begin) * s->esize;
+      return dense_request(s->dtype, flags, base, vals, out, n, st);
+    }
+    PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+    int rc;
+    switch (s->dtype) {
+      case PSG_F32: rc = run_dense_keyed<PSG_F32>(s, flags, keys, vals, out, n, st); break;
+      case PSG_F64: rc = run_dense_keyed<PSG_F64>(s, flags, keys, vals, out, n, st); break;
+      case PSG_F16: rc = run_dense_keyed<PSG_F16>(s, flags, keys, vals, out, n, st); break;
+      default: rc = run_dense_keyed<PSG_BF16>(s, flags, keys, vals, out, n, st); break;
+    }
+    PSG_TRY(rc);
+    PSG_TRY(read_flags(s, st));
+    PSG_REQUIRE(!s->flags_host[F_UNSORTED], PSG_ERR_INVALID,
+                "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
+    PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE,
+                "request key outside the DENSE store slots (values of in-range keys applied)");
+    return PSG_OK;
+  }
+  // SORTED
+  PSG_REQUIRE(keys, PSG_ERR_INVALID, "SORTED store needs explicit keys");
+  uint64_t base = UINT64_MAX;
+  PSG_TRY(sorted_resolve(s, keys, n, true, &base, st));
+  if (base != UINT64_MAX)
+    return dense_request(s->dtype, flags, (char*)s->vals + base * s->esize, vals, out, n, st);
+  return slot_request(s->dtype, flags, s->vals, s->slots, vals, out, n, st);
+}
+
+int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert, uint32_t* slots,
+                      psg_stream stream) {
+  PSG_REQUIRE(s && slots, PSG_ERR_INVALID, "psg_store_resolve: null argument");
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(keys, PSG_ERR_INVALID, "psg_store_resolve: null keys");
+  hipStream_t st = (hipStream_t)stream;
+  if (s->kind == PSG_STORE_DENSE) {
+    PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+    k_dense_slots<<<grid_n(n, kBlock), kBlock, 0, st>>>(keys, n, s->key_begin, s->capacity, slots,
+                                                         s->flags);
+    PSG_HIP(hipGetLastError());
+    PSG_TRY(read_flags(s, st));
+    PSG_REQUIRE(!s->flags_host[F_UNSORTED], PSG_ERR_INVALID,
+                "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
+    PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE, "key outside the DENSE store slots");
+    return PSG_OK;
+  }
+  PSG_TRY(sorted_resolve(s, keys, n, insert != 0, nullptr, st));
+  PSG_HIP(hipMemcpyAsync(slots, s->slots, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  return PSG_OK;
+}
+
+int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots, const void* vals,
+                           void* out, uint64_t n, psg_stream stream) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_handle_slots: null store");
+  PSG_REQUIRE(flags >= 1 && flags <= 3, PSG_ERR_INVALID, "bad flags %d", flags);
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(slots, PSG_ERR_INVALID, "null slots");
+  PSG_REQUIRE(!(flags & PSG_PUSH) || vals, PSG_ERR_INVALID, "push without vals");
+  PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
+  return slot_request(s->dtype, flags, s->vals, slots, vals, out, n, (hipStream_t)stream);
+}
+
+int psg_store_dump(psg_store* s, uint64_t* keys_host, void* vals_host) {
+  PSG_REQUIRE(s && vals_host, PSG_ERR_INVALID, "psg_store_dump: null argument");
+  PSG_HIP(hipDeviceSynchronize());
+  if (s->size == 0) return PSG_OK;
+  PSG_HIP(hipMemcpy(vals_host, s->vals, s->size * s->esize, hipMemcpyDeviceToHost));
+  if (keys_host) {
+    if (s->kind == PSG_STORE_SORTED) {
+      PSG_HIP(hipMemcpy(keys_host, s->keys, s->size * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    } else {
+      for (uint64_t i = 0; i < s->size; ++i) keys_host[i] = s->key_begin + i;
+    }
+  }
+  return PSG_OK;
+}
+
+}  // extern "C"

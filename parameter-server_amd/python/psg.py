@@ -1,0 +1,371 @@
+"""ctypes binding of the psg C-ABI (include/psg.h) for tests and bench.py.
+
+The product is the C-ABI library ``lib/libpsgpu.so`` (HIP kernels for gfx950);
+this module is a thin, typed wrapper over it.  It never falls back to a CPU
+path: when the library is missing, or a call fails, it raises ``PsgError``.
+
+Functions mirror the reference interfaces named in include/psg.h (paths in the
+reference repository SovietPower/Parameter-Server):
+  Store.handle   -> KVServerDefaultHandle::operator()  src/ps/KVApp.h:435-456
+  slice          -> KVWorker::DefaultSlicer            src/ps/KVApp.h:515-574
+  merge          -> AddPullCB merge                    src/ps/KVApp.h:673-726
+  server_ranges  -> PostOffice::GetServerRanges        src/internal/PostOffice.cpp:211-221
+  Comm.push/pull -> BSP Push (reduce-scatter) / Pull (all-gather) over RCCL
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "PSG_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libpsgpu.so"))
+
+F32, F64, F16, BF16 = 0, 1, 2, 3
+DENSE, SORTED = 0, 1
+PUSH, PULL = 1, 2
+H2D, D2H, D2D = 0, 1, 2
+
+_NP = {F32: np.float32, F64: np.float64, F16: np.float16, BF16: np.uint16}
+_ESIZE = {F32: 4, F64: 8, F16: 2, BF16: 2}
+
+# every symbol include/psg.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "psg_abi_version", "psg_last_error", "psg_device_count", "psg_set_device",
+    "psg_get_device", "psg_device_sync", "psg_malloc", "psg_free", "psg_host_alloc",
+    "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
+    "psg_memset", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
+    "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
+    "psg_event_elapsed_ms", "psg_fill_synth", "psg_fill_keys_arith",
+    "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
+    "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
+    "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
+    "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
+    "psg_adam_create", "psg_adam_destroy", "psg_lr_apply",
+]
+
+
+class PsgError(RuntimeError):
+    def __init__(self, code: int, what: str, msg: str):
+        super().__init__(f"{what} -> status {code}: {msg}")
+        self.code = code
+
+
+class StoreInfo(C.Structure):
+    _fields_ = [("kind", C.c_int), ("dtype", C.c_int), ("key_begin", C.c_uint64),
+                ("key_end", C.c_uint64), ("size", C.c_uint64), ("capacity", C.c_uint64),
+                ("vals", C.c_void_p), ("keys", C.c_void_p)]
+
+
+class Segment(C.Structure):
+    _fields_ = [("vals", C.c_void_p), ("count", C.c_uint64), ("first_key", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libpsgpu.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PsgError(-1, "load", f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        vp, u64, i32, f32, f64 = C.c_void_p, C.c_uint64, C.c_int, C.c_float, C.c_double
+        sig = {
+            "psg_abi_version": ([], i32), "psg_last_error": ([], C.c_char_p),
+            "psg_device_count": ([C.POINTER(i32)], i32), "psg_set_device": ([i32], i32),
+            "psg_get_device": ([C.POINTER(i32)], i32), "psg_device_sync": ([], i32),
+            "psg_malloc": ([C.POINTER(vp), C.c_size_t], i32), "psg_free": ([vp], i32),
+            "psg_host_alloc": ([C.POINTER(vp), C.c_size_t], i32), "psg_host_free": ([vp], i32),
+            "psg_host_register": ([vp, C.c_size_t], i32), "psg_host_unregister": ([vp], i32),
+            "psg_memcpy": ([vp, vp, C.c_size_t, i32, vp], i32),
+            "psg_memset": ([vp, i32, C.c_size_t, vp], i32),
+            "psg_stream_create": ([C.POINTER(vp)], i32), "psg_stream_destroy": ([vp], i32),
+            "psg_stream_sync": ([vp], i32), "psg_event_create": ([C.POINTER(vp)], i32),
+            "psg_event_destroy": ([vp], i32), "psg_event_record": ([vp, vp], i32),
+            "psg_event_sync": ([vp], i32),
+            "psg_event_elapsed_ms": ([vp, vp, C.POINTER(f32)], i32),
+            "psg_fill_synth": ([vp, u64, i32, u64, i32, f64, f64, vp], i32),
+            "psg_fill_keys_arith": ([vp, u64, u64, u64, vp], i32),
+            "psg_store_create": ([i32, i32, u64, u64, u64, C.POINTER(vp)], i32),
+            "psg_store_destroy": ([vp], i32),
+            "psg_store_get_info": ([vp, C.POINTER(StoreInfo)], i32),
+            "psg_store_clear": ([vp, vp], i32),
+            "psg_store_handle": ([vp, i32, vp, u64, vp, vp, u64, vp], i32),
+            "psg_store_resolve": ([vp, vp, u64, i32, vp, vp], i32),
+            "psg_store_handle_slots": ([vp, i32, vp, vp, vp, u64, vp], i32),
+            "psg_store_dump": ([vp, vp, vp], i32),
+            "psg_server_ranges": ([i32, vp, vp], i32),
+            "psg_slice": ([vp, u64, vp, u64, i32, vp, vp, vp, vp, vp], i32),
+            "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
+            "psg_comm_id_bytes": ([], i32), "psg_comm_get_id": ([vp], i32),
+            "psg_comm_init": ([vp, i32, i32, C.POINTER(vp)], i32),
+            "psg_comm_destroy": ([vp], i32),
+            "psg_comm_rank": ([vp, C.POINTER(i32), C.POINTER(i32)], i32),
+            "psg_comm_push": ([vp, vp, vp, u64, vp, vp], i32),
+            "psg_comm_pull": ([vp, vp, vp, u64, vp], i32),
+            "psg_adam_create": ([u64, f64, f64, f64, f64, C.POINTER(vp)], i32),
+            "psg_adam_destroy": ([vp], i32),
+            "psg_lr_apply": ([vp, vp, u64, f32, vp, i32, vp], i32),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise PsgError(rc, what, lib().psg_last_error().decode(errors="replace"))
+
+
+def _call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def _ptr(x) -> int | None:
+    if x is None:
+        return None
+    if isinstance(x, DeviceBuffer):
+        return x.ptr
+    if isinstance(x, int):
+        return x
+    raise TypeError(f"expected DeviceBuffer or int device pointer, got {type(x)}")
+
+
+# ---- runtime -------------------------------------------------------------------
+def device_count() -> int:
+    n = C.c_int(0)
+    _call("psg_device_count", C.byref(n))
+    return n.value
+
+
+def set_device(dev: int) -> None:
+    _call("psg_set_device", dev)
+
+
+def device_sync() -> None:
+    _call("psg_device_sync")
+
+
+class Stream:
+    def __init__(self, null: bool = False):
+        self.handle = C.c_void_p(None)
+        if not null:
+            _call("psg_stream_create", C.byref(self.handle))
+
+    @property
+    def ptr(self):
+        return self.handle.value
+
+    def sync(self) -> None:
+        _call("psg_stream_sync", self.handle)
+
+    def close(self) -> None:
+        if self.handle.value:
+            _call("psg_stream_destroy", self.handle)
+            self.handle = C.c_void_p(None)
+
+
+def _s(stream) -> int | None:
+    return None if stream is None else stream.ptr
+
+
+class Event:
+    def __init__(self):
+        self.handle = C.c_void_p(None)
+        _call("psg_event_create", C.byref(self.handle))
+
+    def record(self, stream=None) -> None:
+        _call("psg_event_record", self.handle, _s(stream))
+
+    def sync(self) -> None:
+        _call("psg_event_sync", self.handle)
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = C.c_float(0)
+        _call("psg_event_elapsed_ms", self.handle, end.handle, C.byref(ms))
+        return ms.value
+
+    def close(self) -> None:
+        if self.handle.value:
+            _call("psg_event_destroy", self.handle)
+            self.handle = C.c_void_p(None)
+
+
+class DeviceBuffer:
+    """Raw HBM allocation (psg_malloc) of ``nbytes``; numpy upload/download."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        h = C.c_void_p(None)
+        _call("psg_malloc", C.byref(h), C.c_size_t(self.nbytes))
+        self.ptr = h.value or 0
+
+    @classmethod
+    def from_numpy(cls, a: np.ndarray, stream=None) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(max(a.nbytes, 1))
+        b.upload(a, stream)
+        return b
+
+    def upload(self, a: np.ndarray, stream=None, offset: int = 0) -> None:
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        if a.nbytes:
+            _call("psg_memcpy", C.c_void_p(self.ptr + offset), a.ctypes.data_as(C.c_void_p),
+                  C.c_size_t(a.nbytes), H2D, _s(stream))
+            Stream.sync(stream) if stream is not None else device_sync()
+
+    def download(self, dtype, count: int, stream=None, offset: int = 0) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            assert offset + out.nbytes <= self.nbytes
+            _call("psg_memcpy", out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr + offset),
+                  C.c_size_t(out.nbytes), D2H, _s(stream))
+            Stream.sync(stream) if stream is not None else device_sync()
+        return out
+
+    def fill_synth(self, n: int, dtype: int, seed: int, mode: int, lo: float, hi: float,
+                   stream=None) -> None:
+        _call("psg_fill_synth", C.c_void_p(self.ptr), n, dtype, seed, mode, lo, hi, _s(stream))
+
+    def free(self) -> None:
+        if self.ptr:
+            _call("psg_free", C.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# ---- value store ----------------------------------------------------------------
+class Store:
+    """One server shard's value store in HBM (psg_store_*)."""
+
+    def __init__(self, kind: int, dtype: int, key_begin: int, key_end: int, capacity: int):
+        self.h = C.c_void_p(None)
+        _call("psg_store_create", kind, dtype, key_begin, key_end, capacity, C.byref(self.h))
+        self.dtype = dtype
+        self.esize = _ESIZE[dtype]
+
+    def info(self) -> StoreInfo:
+        i = StoreInfo()
+        _call("psg_store_get_info", self.h, C.byref(i))
+        return i
+
+    def handle(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> None:
+        _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,
+              _s(stream))
+
+    def resolve(self, keys, n: int, slots, insert: bool = True, stream=None) -> None:
+        _call("psg_store_resolve", self.h, _ptr(keys), n, int(insert), _ptr(slots), _s(stream))
+
+    def handle_slots(self, flags: int, slots, vals, out, n: int, stream=None) -> None:
+        _call("psg_store_handle_slots", self.h, flags, _ptr(slots), _ptr(vals), _ptr(out), n,
+              _s(stream))
+
+    def clear(self, stream=None) -> None:
+        _call("psg_store_clear", self.h, _s(stream))
+
+    def dump(self):
+        i = self.info()
+        keys = np.empty(i.size, dtype=np.uint64)
+        vals = np.empty(i.size, dtype=_NP[self.dtype])
+        _call("psg_store_dump", self.h, keys.ctypes.data_as(C.c_void_p),
+              vals.ctypes.data_as(C.c_void_p))
+        return keys, vals
+
+    def close(self) -> None:
+        if self.h.value:
+            _call("psg_store_destroy", self.h)
+            self.h = C.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- worker side --------------------------------------------------------------
+def server_ranges(ns: int):
+    b = np.empty(ns, dtype=np.uint64)
+    e = np.empty(ns, dtype=np.uint64)
+    _call("psg_server_ranges", ns, b.ctypes.data_as(C.c_void_p), e.ctypes.data_as(C.c_void_p))
+    return b, e
+
+
+def slice_keys(keys, n: int, begins: np.ndarray, ends: np.ndarray, lens=None, num_vals=None,
+               stream=None):
+    ns = len(begins)
+    begins = np.ascontiguousarray(begins, dtype=np.uint64)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    kp = np.empty(ns + 1, dtype=np.uint64)
+    vp = np.empty(ns + 1, dtype=np.uint64)
+    _call("psg_slice", _ptr(keys), n, _ptr(lens), n if num_vals is None else num_vals, ns,
+          begins.ctypes.data_as(C.c_void_p), ends.ctypes.data_as(C.c_void_p),
+          kp.ctypes.data_as(C.c_void_p), vp.ctypes.data_as(C.c_void_p), _s(stream))
+    return kp, vp
+
+
+def merge(segments, elem_size: int, dst, dst_count: int, stream=None) -> None:
+    """segments: list of (device ptr or DeviceBuffer, count, first_key)."""
+    arr = (Segment * max(len(segments), 1))()
+    for i, (p, cnt, fk) in enumerate(segments):
+        arr[i].vals = _ptr(p)
+        arr[i].count = cnt
+        arr[i].first_key = fk
+    _call("psg_merge", arr, len(segments), elem_size, _ptr(dst), dst_count, _s(stream))
+
+
+# ---- multi-GPU ------------------------------------------------------------------
+def comm_id() -> bytes:
+    n = lib().psg_comm_id_bytes()
+    buf = C.create_string_buffer(n)
+    _call("psg_comm_get_id", buf)
+    return buf.raw
+
+
+class Comm:
+    def __init__(self, uid: bytes, nranks: int, rank: int):
+        self.h = C.c_void_p(None)
+        buf = C.create_string_buffer(uid, len(uid))
+        _call("psg_comm_init", buf, nranks, rank, C.byref(self.h))
+
+    def push(self, shard: Store, vals, n_total: int, scratch=None, stream=None) -> None:
+        _call("psg_comm_push", self.h, shard.h, _ptr(vals), n_total, _ptr(scratch), _s(stream))
+
+    def pull(self, shard: Store, out, n_total: int, stream=None) -> None:
+        _call("psg_comm_pull", self.h, shard.h, _ptr(out), n_total, _s(stream))
+
+    def close(self) -> None:
+        if self.h.value:
+            _call("psg_comm_destroy", self.h)
+            self.h = C.c_void_p(None)
+
+
+# ---- LR -----------------------------------------------------------------------
+class Adam:
+    def __init__(self, n: int, lr: float, beta1=0.9, beta2=0.999, eps=1e-8):
+        self.h = C.c_void_p(None)
+        _call("psg_adam_create", n, lr, beta1, beta2, eps, C.byref(self.h))
+
+    def close(self) -> None:
+        if self.h.value:
+            _call("psg_adam_destroy", self.h)
+            self.h = C.c_void_p(None)
+
+
+def lr_apply(weights: Store, merged, n: int, lr: float, adam: Adam | None, iteration: int,
+             stream=None) -> None:
+    _call("psg_lr_apply", weights.h, _ptr(merged), n, lr, adam.h if adam else None, iteration,
+          _s(stream))

@@ -1,0 +1,305 @@
+"""Parity of the HIP path (through the psg C-ABI) with the CPU oracle.
+
+Bar: bit-exact for every integer / index result and for the float sums of the
+reference's integer-valued test data; real-valued f32 sums are also bit-exact
+here because both sides add the same two operands in the same order per
+request (the tolerance the north star allows, 1e-6 relative, is asserted where
+orders may differ: tests/test_dist.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import psg
+from kv_pipeline import GpuKV, run_kv_app, run_my
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = np.load(os.path.join(HERE, "golden", "golden.npz"))
+KMAX = (1 << 64) - 1
+NPT = {psg.F32: np.float32, psg.F64: np.float64, psg.F16: np.uint16, psg.BF16: np.uint16}
+ES = {psg.F32: 4, psg.F64: 8, psg.F16: 2, psg.BF16: 2}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    assert psg.device_count() >= 1, "no GPU visible"
+    psg.set_device(0)
+    yield
+
+
+def dev(a):
+    return psg.DeviceBuffer.from_numpy(a)
+
+
+def synth(n, dtype, seed, mode=0, lo=0.0, hi=1000.0):
+    return oracle.synth(n, dtype, seed, mode, lo, hi)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64, psg.F16, psg.BF16])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_synth_generator_bitexact(dtype, mode):
+    n = 100003
+    b = psg.DeviceBuffer(n * ES[dtype])
+    lo, hi = (0.0, 1000.0) if mode == 0 else (-1.0, 1.0)
+    b.fill_synth(n, dtype, 77, mode, lo, hi)
+    got = b.download(NPT[dtype], n)
+    np.testing.assert_array_equal(got, oracle.synth(n, dtype, 77, mode, lo, hi))
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64, psg.F16, psg.BF16])
+@pytest.mark.parametrize("n,off", [(1, 0), (3, 1), (1000, 0), (4099, 5), (65536, 3), (262147, 0)])
+def test_dense_requests_vs_oracle(dtype, n, off):
+    kb = 1000
+    cap = n + off + 7
+    st = psg.Store(psg.DENSE, dtype, kb, kb + cap + 100, cap)
+    orc = oracle.Store(dtype)
+    mode = 1 if dtype in (psg.F32, psg.F64) else 0
+    v1 = synth(n, dtype, 1, mode, -1.0 if mode else 0.0, 1.0 if mode else 1000.0)
+    v2 = synth(n, dtype, 2, mode, -1.0 if mode else 0.0, 1.0 if mode else 1000.0)
+    d1, d2 = dev(v1), dev(v2)
+    out = psg.DeviceBuffer(n * ES[dtype])
+    fk = kb + off
+    st.handle(psg.PUSH, None, d1, None, n, first_key=fk)
+    orc.handle(oracle.PUSH, None, v1, n, first_key=fk)
+    st.handle(psg.PUSH | psg.PULL, None, d2, out, n, first_key=fk)
+    exp = orc.handle(oracle.PUSH | oracle.PULL, None, v2, n, first_key=fk)
+    np.testing.assert_array_equal(out.download(NPT[dtype], n), exp)
+    st.handle(psg.PULL, None, None, out, n, first_key=fk)
+    exp = orc.handle(oracle.PULL, None, None, n, first_key=fk)
+    np.testing.assert_array_equal(out.download(NPT[dtype], n), exp)
+    # untouched slots stayed zero
+    _, vals = st.dump()
+    assert not np.any(vals[:off].view(np.uint8)) and not np.any(vals[off + n:].view(np.uint8))
+
+
+def test_dense_full_size_64m_integer_exact():
+    """configs[1] size: 64 M floats, integer-valued, so every sum is exact."""
+    n = 64 << 20
+    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
+    v = psg.DeviceBuffer(n * 4)
+    v.fill_synth(n, psg.F32, 7, 0, 0.0, 1000.0)
+    out = psg.DeviceBuffer(n * 4)
+    for _ in range(3):
+        st.handle(psg.PUSH, None, v, None, n)
+    st.handle(psg.PULL, None, None, out, n)
+    host_v = v.download(np.float32, n)
+    np.testing.assert_array_equal(out.download(np.float32, n), host_v * 3)
+    st.handle(psg.PUSH | psg.PULL, None, v, out, n)
+    np.testing.assert_array_equal(out.download(np.float32, n), host_v * 4)
+    # spot check against the generator's restatement
+    np.testing.assert_array_equal(host_v[:4096], oracle.synth(4096, oracle.F32, 7, 0, 0.0, 1000.0))
+
+
+def test_dense_keyed_requests():
+    kb = 50
+    st = psg.Store(psg.DENSE, psg.F32, kb, 10_000, 4096)
+    orc = oracle.Store()
+    rng = np.random.default_rng(3)
+    keys = np.unique(rng.integers(kb, kb + 4096, 1500)).astype(np.uint64)
+    v = rng.uniform(-1, 1, len(keys)).astype(np.float32)
+    out = psg.DeviceBuffer(len(keys) * 4)
+    st.handle(psg.PUSH | psg.PULL, dev(keys), dev(v), out, len(keys))
+    exp = orc.handle(oracle.PUSH | oracle.PULL, keys, v, len(keys))
+    np.testing.assert_array_equal(out.download(np.float32, len(keys)), exp)
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(np.array([kb + 5000], np.uint64)), dev(v[:1]), None, 1)
+    assert ei.value.code == 4  # PSG_ERR_RANGE
+
+
+# ---------------------------------------------------------------------------
+def _sorted_sequence(n_univ, seed):
+    rng = np.random.default_rng(seed)
+    univ = np.unique(rng.integers(1 << 40, 1 << 62, n_univ, dtype=np.uint64))
+    reqs = []
+    for r in range(8):
+        k = np.sort(rng.choice(univ, size=rng.integers(1, len(univ)), replace=False))
+        flags = [psg.PUSH, psg.PULL, psg.PUSH | psg.PULL][r % 3]
+        reqs.append((flags, k.astype(np.uint64), rng.uniform(-1, 1, len(k)).astype(np.float32)))
+    reqs.append((psg.PUSH, univ, rng.uniform(-1, 1, len(univ)).astype(np.float32)))
+    reqs.append((psg.PUSH | psg.PULL, univ, rng.uniform(-1, 1, len(univ)).astype(np.float32)))
+    return reqs
+
+
+@pytest.mark.parametrize("n_univ,seed", [(50, 1), (5000, 2), (300000, 3)])
+def test_sorted_store_vs_oracle(n_univ, seed):
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    for flags, k, v in _sorted_sequence(n_univ, seed):
+        n = len(k)
+        out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+        st.handle(flags, dev(k), dev(v) if flags & psg.PUSH else None, out, n)
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
+        if out is not None:
+            np.testing.assert_array_equal(out.download(np.float32, n), exp)
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)  # pulls of absent keys inserted them too
+    np.testing.assert_array_equal(gv, ov)
+
+
+def test_sorted_store_benchmark_layout():
+    """test_kv_app_benchmark keys (kMaxKey/num*i + rank): first Push inserts, then dense fast path."""
+    num = 1 << 20
+    keys = (np.arange(num, dtype=np.uint64) * np.uint64(KMAX // num)).astype(np.uint64)
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    v = psg.DeviceBuffer(num * 4)
+    v.fill_synth(num, psg.F32, 9, 0, 0.0, 1000.0)
+    dk = dev(keys)
+    for _ in range(3):
+        st.handle(psg.PUSH, dk, v, None, num)
+    out = psg.DeviceBuffer(num * 4)
+    st.handle(psg.PULL, dk, None, out, num)
+    np.testing.assert_array_equal(out.download(np.float32, num), v.download(np.float32, num) * 3)
+    assert st.info().size == num
+
+
+def test_sorted_resolve_and_slot_requests():
+    rng = np.random.default_rng(11)
+    keys = np.unique(rng.integers(0, 1 << 63, 20000, dtype=np.uint64))
+    n = len(keys)
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    slots = psg.DeviceBuffer(n * 4)
+    st.resolve(dev(keys), n, slots, insert=True)  # inserts, like operator[]
+    s = slots.download(np.uint32, n)
+    assert sorted(s.tolist()) == list(range(n))
+    v = rng.uniform(-1, 1, n).astype(np.float32)
+    out = psg.DeviceBuffer(n * 4)
+    for _ in range(2):
+        st.handle_slots(psg.PUSH | psg.PULL, slots, dev(v), out, n)
+        exp = orc.handle(oracle.PUSH | oracle.PULL, keys, v, n)
+        np.testing.assert_array_equal(out.download(np.float32, n), exp)
+    # resolve without insert: absent keys -> UINT32_MAX
+    more = np.array([keys[0], keys[0] + 1], dtype=np.uint64)
+    st.resolve(dev(more), 2, slots, insert=False)
+    s2 = slots.download(np.uint32, 2)
+    assert s2[1] == 0xFFFFFFFF and s2[0] != 0xFFFFFFFF
+
+
+def test_sorted_rejects_unsorted_and_out_of_range():
+    st = psg.Store(psg.SORTED, psg.F32, 100, 200, 0)
+    v = dev(np.ones(3, np.float32))
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(np.array([150, 120, 160], np.uint64)), v, None, 3)
+    assert ei.value.code == 1
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(np.array([150, 199, 200], np.uint64)), v, None, 3)
+    assert ei.value.code == 4
+
+
+# ---------------------------------------------------------------------------
+def test_slice_golden_cases():
+    for j in range(int(G["slice_ncases"][0])):
+        keys = G[f"slice{j}_keys"]
+        ns = int(G[f"slice{j}_ns"][0])
+        haslens = bool(G[f"slice{j}_haslens"][0])
+        b, e = psg.server_ranges(ns)
+        lens = dev(G[f"slice{j}_lens"]) if haslens else None
+        kp, vp = psg.slice_keys(dev(keys), len(keys), b, e, lens=lens,
+                                num_vals=None if haslens else len(keys))
+        np.testing.assert_array_equal(kp, G[f"slice{j}_kpos"], err_msg=f"case {j}")
+        np.testing.assert_array_equal(vp, G[f"slice{j}_vpos"], err_msg=f"case {j}")
+
+
+@pytest.mark.parametrize("n,ns", [(1, 1), (1000, 3), (1 << 20, 8), (10_000_000, 4)])
+def test_slice_vs_oracle_large(n, ns):
+    rng = np.random.default_rng(n + ns)
+    keys = np.unique(rng.integers(0, KMAX, n, dtype=np.uint64))
+    lens = rng.integers(0, 4, len(keys)).astype(np.int32)
+    b, e = psg.server_ranges(ns)
+    dk = dev(keys)
+    kp, vp = psg.slice_keys(dk, len(keys), b, e, lens=dev(lens))
+    okp, ovp = oracle.slice_keys(keys, b, e, lens)
+    np.testing.assert_array_equal(kp, okp)
+    np.testing.assert_array_equal(vp, ovp)
+    kp2, vp2 = psg.slice_keys(dk, len(keys), b, e, num_vals=2 * len(keys))
+    okp2, ovp2 = oracle.slice_keys(keys, b, e, num_vals=2 * len(keys))
+    np.testing.assert_array_equal(kp2, okp2)
+    np.testing.assert_array_equal(vp2, ovp2)
+
+
+def test_slice_rejects_key_past_last_range():
+    b, e = psg.server_ranges(4)
+    with pytest.raises(psg.PsgError):
+        psg.slice_keys(dev(np.array([3, KMAX], np.uint64)), 2, b, e)
+
+
+@pytest.mark.parametrize("esize,dtype", [(4, np.float32), (2, np.uint16), (8, np.float64)])
+def test_merge_vs_oracle(esize, dtype):
+    rng = np.random.default_rng(esize)
+    counts = [0, 1, 7, 1000, 4096, 33, 100003]
+    segs_host = [(rng.integers(0, 1 << 15, c).astype(dtype), int(rng.integers(0, KMAX, dtype=np.uint64)))
+                 for c in counts]
+    total = sum(counts)
+    segs_dev = [(dev(a) if len(a) else psg.DeviceBuffer(0), len(a), fk) for a, fk in segs_host]
+    dst = psg.DeviceBuffer(total * esize + 4)
+    psg.merge(segs_dev, esize, dst, total)
+    exp = oracle.merge(segs_host, total, dtype=dtype)
+    np.testing.assert_array_equal(dst.download(dtype, total), exp)
+    # misaligned destination (byte offset not a multiple of 16)
+    psg.merge(segs_dev, esize, dst.ptr + esize, total)
+    np.testing.assert_array_equal(dst.download(dtype, total, offset=esize), exp)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("ns", [1, 2, 4])
+def test_kat_test_kv_app_on_gpu(ns):
+    """tests/test_kv_app.cpp:20-61 through GPU slice + SORTED stores + GPU merge."""
+    rets, outs = run_kv_app(GpuKV(ns), G["kv_app_keys"], G["kv_app_vals"])
+    np.testing.assert_array_equal(rets, G["kv_app_rets"])
+    np.testing.assert_array_equal(outs, G["kv_app_outs"])
+
+
+def test_kat_test_my_on_gpu():
+    rets, final = run_my(GpuKV(3), G["my_keys"], [G[f"my{c}_vals"] for c in range(3)])
+    np.testing.assert_array_equal(rets, G["my_rets"])
+    np.testing.assert_array_equal(final, G["my_final"])
+
+
+def test_kat_multi_workers_on_gpu():
+    kv = GpuKV(2)
+    for c in (0, 1):
+        rets, outs = run_kv_app(kv, G[f"mw{c}_keys"], G[f"mw{c}_vals"])
+        np.testing.assert_array_equal(rets, G[f"mw{c}_rets"])
+        np.testing.assert_array_equal(outs, G[f"mw{c}_outs"])
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("adam", [False, True])
+def test_lr_apply_bitexact(adam):
+    n = 100003
+    rng = np.random.default_rng(8)
+    w0 = rng.uniform(-0.5, 0.5, n).astype(np.float32)
+    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
+    st.handle(psg.PUSH, None, dev(w0), None, n)
+    a = psg.Adam(n, 0.01) if adam else None
+    w = w0.copy()
+    m = np.zeros(n) if adam else None
+    v = np.zeros(n) if adam else None
+    for it in range(4):
+        merged = rng.uniform(-1, 1, n).astype(np.float32)
+        psg.lr_apply(st, dev(merged), n, 0.01, a, it)
+        oracle.lr_apply(w, merged, 0.01, m, v, float(np.float32(0.01)), 0.9, 0.999, 1e-8, it)
+    _, got = st.dump()
+    np.testing.assert_array_equal(got, w)
+
+
+def test_comm_single_rank_push_pull():
+    uid = psg.comm_id()
+    c = psg.Comm(uid, 1, 0)
+    n = 1 << 20
+    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
+    v = psg.DeviceBuffer(n * 4)
+    v.fill_synth(n, psg.F32, 3, 0, 0.0, 1000.0)
+    out = psg.DeviceBuffer(n * 4)
+    c.push(st, v, n)
+    c.push(st, v, n)
+    c.pull(st, out, n)
+    np.testing.assert_array_equal(out.download(np.float32, n), v.download(np.float32, n) * 2)
+    c.close()
