@@ -238,7 +238,7 @@ def test_merge_vs_oracle(esize, dtype):
                  for c in counts]
     total = sum(counts)
     segs_dev = [(dev(a) if len(a) else psg.DeviceBuffer(0), len(a), fk) for a, fk in segs_host]
-    dst = psg.DeviceBuffer(total * esize + 4)
+    dst = psg.DeviceBuffer(total * esize + 16)
     psg.merge(segs_dev, esize, dst, total)
     exp = oracle.merge(segs_host, total, dtype=dtype)
     np.testing.assert_array_equal(dst.download(dtype, total), exp)
