@@ -45,25 +45,25 @@ __global__ __launch_bounds__(256) void k_dense_vec(u32x4* __restrict__ store,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint64_t i = base + (uint64_t)u * kBlock;
-        if constexpr ((OP & PSG_PUSH) != 0) v[u] = ld16<NT>(vals + i);
-        s[u] = ld16<0>(store + i);
+        if constexpr ((OP & PSG_PUSH) != 0) v[u] = ld16<NT & 1>(vals + i);
+        s[u] = ld16<(NT >> 1) & 1>(store + i);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint64_t i = base + (uint64_t)u * kBlock;
         if constexpr ((OP & PSG_PUSH) != 0) {
           s[u] = E::add(s[u], v[u]);
-          st16<0>(store + i, s[u]);
+          st16<(NT >> 1) & 1>(store + i, s[u]);
         }
-        if constexpr ((OP & PSG_PULL) != 0) st16<NT>(out + i, s[u]);
+        if constexpr ((OP & PSG_PULL) != 0) st16<NT & 1>(out + i, s[u]);
       }
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint64_t i = base + (uint64_t)u * kBlock;
         if (i < nvec) {
-          if constexpr ((OP & PSG_PUSH) != 0) v[u] = ld16<NT>(vals + i);
-          s[u] = ld16<0>(store + i);
+          if constexpr ((OP & PSG_PUSH) != 0) v[u] = ld16<NT & 1>(vals + i);
+          s[u] = ld16<(NT >> 1) & 1>(store + i);
         }
       }
 #pragma unroll
@@ -72,9 +72,9 @@ __global__ __launch_bounds__(256) void k_dense_vec(u32x4* __restrict__ store,
         if (i < nvec) {
           if constexpr ((OP & PSG_PUSH) != 0) {
             s[u] = E::add(s[u], v[u]);
-            st16<0>(store + i, s[u]);
+            st16<(NT >> 1) & 1>(store + i, s[u]);
           }
-          if constexpr ((OP & PSG_PULL) != 0) st16<NT>(out + i, s[u]);
+          if constexpr ((OP & PSG_PULL) != 0) st16<NT & 1>(out + i, s[u]);
         }
       }
     }
@@ -125,9 +125,9 @@ __global__ __launch_bounds__(256) void k_slots(typename Elem<DT>::T* __restrict_
 // ---- tuning knobs (fixed defaults; env overrides exist for the sweep in
 // tools/sweep_dense.py only) ---------------------------------------------------
 struct DenseCfg {
-  int unroll = 4;
+  int unroll = 2;
   int nt = 1;
-  int blocks_per_cu = 8;
+  int blocks_per_cu = 4;
 };
 static DenseCfg dense_cfg() {
   static DenseCfg cfg = [] {
@@ -137,7 +137,7 @@ static DenseCfg dense_cfg() {
     if (const char* e = getenv("PSG_DENSE_BPC")) c.blocks_per_cu = atoi(e);
     if (c.unroll != 1 && c.unroll != 2 && c.unroll != 4 && c.unroll != 8) c.unroll = 4;
     if (c.blocks_per_cu < 1 || c.blocks_per_cu > 32) c.blocks_per_cu = 8;
-    c.nt = c.nt ? 1 : 0;
+    if (c.nt < 0 || c.nt > 3) c.nt = 1;
     return c;
   }();
   return cfg;
@@ -168,7 +168,8 @@ static void dispatch_vec(const DenseCfg& c, void* store, const void* vals, void*
     launch_vec<DT, OP, U, NT>(store, vals, out, nvec, c.blocks_per_cu, s); \
     return;                                                               \
   }
-  PSG_V(1, 0) PSG_V(1, 1) PSG_V(2, 0) PSG_V(2, 1) PSG_V(4, 0) PSG_V(4, 1) PSG_V(8, 0) PSG_V(8, 1)
+  PSG_V(1, 0) PSG_V(1, 1) PSG_V(1, 2) PSG_V(1, 3) PSG_V(2, 0) PSG_V(2, 1) PSG_V(2, 2) PSG_V(2, 3)
+  PSG_V(4, 0) PSG_V(4, 1) PSG_V(4, 2) PSG_V(4, 3) PSG_V(8, 0) PSG_V(8, 1) PSG_V(8, 2) PSG_V(8, 3)
 #undef PSG_V
 }
 

@@ -278,7 +278,9 @@ def test_lr_apply_bitexact(adam):
     w0 = rng.uniform(-0.5, 0.5, n).astype(np.float32)
     st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
     st.handle(psg.PUSH, None, dev(w0), None, n)
-    a = psg.Adam(n, 0.01) if adam else None
+    # LRServer constructs Adam from its float learning_rate_ (LRServer.h:83-84), so the
+    # Adam learning rate is the f32 0.01 widened to double, as the oracle gets it.
+    a = psg.Adam(n, float(np.float32(0.01))) if adam else None
     w = w0.copy()
     m = np.zeros(n) if adam else None
     v = np.zeros(n) if adam else None

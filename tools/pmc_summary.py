@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes.
+
+usage: pmc_summary.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEYS OUT_JSON
+
+FETCH_DIR / WRITE_DIR are the -d output directories of
+  rocprofv3 --pmc FETCH_SIZE --output-format csv ...
+  rocprofv3 --pmc WRITE_SIZE --output-format csv ...
+(separate passes: FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2, MI355X_MICROARCH.md
+"rocprofv3 PMC slots").  Units are KiB.  gfx950 correction (MI355X_MICROARCH.md
+"HBM"): FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming
+read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+  hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   per launch (median).
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def read_counter(d, kernel_sub, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = {}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel_sub not in row.get("Kernel_Name", ""):
+                    continue
+                if row.get("Counter_Name") != counter:
+                    continue
+                key = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals))
+                vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    fdir, wdir, ksub, keys, out = sys.argv[1:6]
+    fetch = read_counter(fdir, ksub, "FETCH_SIZE")
+    write = read_counter(wdir, ksub, "WRITE_SIZE")
+    if not fetch or not write:
+        print("no counter rows found", len(fetch), len(write))
+        sys.exit(1)
+    f = statistics.median(fetch)
+    w = statistics.median(write)
+    hbm = (2 * f + w) * 1024
+    res = {
+        "kernel": ksub,
+        "keys": int(keys),
+        "fetch_size_kib_median": f,
+        "write_size_kib_median": w,
+        "launches": [len(fetch), len(write)],
+        "correction": "gfx950: FETCH_SIZE x2 (wide streaming reads), WRITE_SIZE x1; KiB -> bytes",
+        "hbm_bytes_per_launch": int(hbm),
+        "alg_bytes_per_launch": 12 * int(keys),
+        "traffic_over_alg": hbm / (12 * int(keys)),
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
