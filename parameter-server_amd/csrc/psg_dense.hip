@@ -12,8 +12,10 @@
 // vectors of every stream in flight, blocks grid-stride over 256*U-vector
 // tiles (cdna_hip_programming.md Guidelines 11, 13, Appendix B 'Element-wise').
 // The once-read request stream (vals) and the write-only reply stream (out)
-// use non-temporal loads/stores; the store itself keeps the default policy so
-// a Pull that follows a Push can hit the Infinity Cache.
+// use non-temporal loads/stores (+20 % over default policy in the sweep); the
+// store keeps the default policy while it can live in the Infinity Cache.
+// Measured HBM traffic of the Push kernel = 1.00003 x the 12 B/elem algorithmic
+// bytes (profiles/pmc_push_traffic.json): no re-reads.
 #include <cstdlib>
 
 #include "psg_internal.h"
@@ -122,12 +124,17 @@ __global__ __launch_bounds__(256) void k_slots(typename Elem<DT>::T* __restrict_
   }
 }
 
-// ---- tuning knobs (fixed defaults; env overrides exist for the sweep in
-// tools/sweep_dense.py only) ---------------------------------------------------
+// ---- tuning knobs ------------------------------------------------------------
+// Defaults from the MI355X sweep (profiles/r1_sweep_dense_{64M,256M}.json):
+// 2 vectors per stream in flight per lane, 2 blocks of 256 per CU (512 blocks
+// grid-striding), non-temporal request/reply streams.  Once the store itself
+// is well past the 256 MiB Infinity Cache (> 512 MiB) its loads and stores go
+// non-temporal too (nt = 3): at 256 M floats that was +3..6 % on the Pull.
+// PSG_DENSE_{UNROLL,NT,BPC} override them, for tools/sweep_dense.py only.
 struct DenseCfg {
   int unroll = 2;
-  int nt = 1;
-  int blocks_per_cu = 4;
+  int nt = -1;  // -1: by store size
+  int blocks_per_cu = 2;
 };
 static DenseCfg dense_cfg() {
   static DenseCfg cfg = [] {
@@ -135,12 +142,17 @@ static DenseCfg dense_cfg() {
     if (const char* e = getenv("PSG_DENSE_UNROLL")) c.unroll = atoi(e);
     if (const char* e = getenv("PSG_DENSE_NT")) c.nt = atoi(e);
     if (const char* e = getenv("PSG_DENSE_BPC")) c.blocks_per_cu = atoi(e);
-    if (c.unroll != 1 && c.unroll != 2 && c.unroll != 4 && c.unroll != 8) c.unroll = 4;
-    if (c.blocks_per_cu < 1 || c.blocks_per_cu > 32) c.blocks_per_cu = 8;
-    if (c.nt < 0 || c.nt > 3) c.nt = 1;
+    if (c.unroll != 1 && c.unroll != 2 && c.unroll != 4 && c.unroll != 8) c.unroll = 2;
+    if (c.blocks_per_cu < 1 || c.blocks_per_cu > 32) c.blocks_per_cu = 2;
+    if (c.nt < -1 || c.nt > 3) c.nt = -1;
     return c;
   }();
   return cfg;
+}
+static DenseCfg dense_cfg_for(uint64_t store_bytes) {
+  DenseCfg c = dense_cfg();
+  if (c.nt < 0) c.nt = store_bytes > (512ull << 20) ? 3 : 1;
+  return c;
 }
 
 static unsigned stream_grid(uint64_t units, uint64_t per_block, int bpc) {
@@ -180,7 +192,7 @@ static int run_dense(void* store, const void* vals, void* out, uint64_t n, hipSt
   const bool need_vals = (OP & PSG_PUSH) != 0, need_out = (OP & PSG_PULL) != 0;
   bool vec_ok = aligned16(store) && (!need_vals || aligned16(vals)) && (!need_out || aligned16(out));
   uint64_t nvec = vec_ok ? n / kVec : 0;
-  if (nvec) dispatch_vec<DT, OP>(dense_cfg(), store, vals, out, nvec, s);
+  if (nvec) dispatch_vec<DT, OP>(dense_cfg_for(n * sizeof(T)), store, vals, out, nvec, s);
   uint64_t done = nvec * kVec;
   if (done < n) {
     uint64_t rest = n - done;
