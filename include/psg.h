@@ -94,6 +94,8 @@ int psg_device_count(int* n);
 int psg_set_device(int device);
 int psg_get_device(int* device);
 int psg_device_sync(void);
+/* Let kernels on `device` read/write `peer`'s HBM over xGMI (idempotent). */
+int psg_enable_peer_access(int device, int peer);
 
 int psg_malloc(void** dptr, size_t bytes);
 int psg_free(void* dptr);

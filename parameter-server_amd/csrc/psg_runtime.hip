@@ -103,6 +103,20 @@ int psg_device_sync(void) {
   PSG_HIP(hipDeviceSynchronize());
   return PSG_OK;
 }
+int psg_enable_peer_access(int device, int peer) {
+  if (device == peer) return PSG_OK;
+  int cur = 0, can = 0;
+  PSG_HIP(hipGetDevice(&cur));
+  PSG_HIP(hipDeviceCanAccessPeer(&can, device, peer));
+  PSG_REQUIRE(can, PSG_ERR_UNSUPPORTED, "GPU %d cannot access GPU %d", device, peer);
+  PSG_HIP(hipSetDevice(device));
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+  (void)hipSetDevice(cur);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+    return hip_fail(e, "hipDeviceEnablePeerAccess", __FILE__, __LINE__);
+  return PSG_OK;
+}
 
 int psg_malloc(void** dptr, size_t bytes) {
   PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_malloc: null out");

@@ -1,0 +1,93 @@
+// internal/customer.h — per-app receive thread and request tracker (reference
+// src/internal/Customer.{h,cpp}, ThreadsafePQueue.h).
+//
+// One receive thread per app object runs the app's handle for every incoming
+// message in priority order (FIFO among equal priorities — the reference's
+// `<=` comparator is not a strict weak ordering), then,
+// for a response, bumps the request tracker (the handle runs BEFORE the bump,
+// Customer.cpp:58-67, which KVWorker::OnReceive relies on).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <thread>
+#include <vector>
+
+#include "internal/message.h"
+
+namespace ps {
+
+class PostOffice;
+
+class ThreadsafePQueue {
+ public:
+  void Push(Message msg) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      msg.meta.seq = next_seq_++;
+      queue_.push(std::move(msg));
+    }
+    cv_.notify_one();
+  }
+  Message WaitAndPop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [this] { return !queue_.empty(); });
+    Message m = queue_.top();
+    queue_.pop();
+    return m;
+  }
+
+ private:
+  struct Cmp {
+    bool operator()(const Message& a, const Message& b) const {
+      if (a.meta.priority != b.meta.priority) return a.meta.priority < b.meta.priority;
+      return a.meta.seq > b.meta.seq;
+    }
+  };
+  std::mutex mu_;
+  std::condition_variable cv_;
+  uint64_t next_seq_ = 0;
+  std::priority_queue<Message, std::vector<Message>, Cmp> queue_;
+};
+
+class Customer {
+ public:
+  using ReceiveHandle = std::function<void(const Message& received)>;
+
+  Customer(int app_id, int customer_id, const ReceiveHandle& handle);
+  ~Customer();
+  Customer(const Customer&) = delete;
+  Customer& operator=(const Customer&) = delete;
+
+  /* new request to `receiver` (a node id or group): tracker entry expects one
+   * response per node (Customer.cpp:22-27) */
+  int NewRequest(int receiver);
+  void WaitRequest(int request_id);
+  int GetResponse(int request_id);
+  void AddResponse(int request_id, int cnt = 1);
+  /* called by the Van for every data message to this customer */
+  void OnReceive(const Message& received) { receive_queue_.Push(received); }
+
+  int app_id() const { return app_id_; }
+  int customer_id() const { return customer_id_; }
+  PostOffice* post_office() const { return po_; }
+
+ private:
+  void ReceiveThread();
+
+  int app_id_;
+  int customer_id_;
+  PostOffice* po_;
+  ReceiveHandle receive_handle_;
+  ThreadsafePQueue receive_queue_;
+  std::unique_ptr<std::thread> receive_thread_;
+  // tracker_[ts] = (expected responses, received responses)
+  std::vector<std::pair<int, int>> tracker_;
+  std::condition_variable tracker_cond_;
+  std::mutex tracker_mu_;
+};
+
+}  // namespace ps

@@ -1,0 +1,52 @@
+// internal/van.h — the transport seam (reference src/internal/Van.h:25-111).
+//
+// The reference's Van moves protobuf-framed ZeroMQ multipart messages between
+// processes (ZMQVan.cpp:147-248).  On one MI355X node this runtime keeps every
+// node of the job in one process, one thread per node, so a Van hands the
+// Message — frames included, host or HBM, zero-copy — straight to the
+// receiver's Customer queue.  HBM frames stay where they are: the receiving
+// node's kernels read them over xGMI (peer access is enabled between all GPUs
+// at start-up).  Selected by PS_VAN_TYPE ("local", the default).
+#pragma once
+#include <atomic>
+#include <memory>
+#include <string>
+
+#include "internal/message.h"
+
+namespace ps {
+
+class PostOffice;
+
+class Van {
+ public:
+  static Van* Create(const std::string& type, PostOffice* po);
+  virtual ~Van() = default;
+
+  virtual void Start(int customer_id);
+  virtual void Stop();
+  /* send a message; fills meta.sender; returns bytes sent (Van.cpp:170-179) */
+  int Send(const Message& msg);
+  const Node& my_node() const { return my_node_; }
+  bool IsReady() const { return ready_.load(); }
+  int GetAvailableTimestamp() { return timestamp_++; }
+  uint64_t send_bytes() const { return send_bytes_.load(); }
+  uint64_t receive_bytes() const { return receive_bytes_.load(); }
+  void CountReceived(uint64_t b) { receive_bytes_ += b; }
+
+ protected:
+  explicit Van(PostOffice* po);
+  /* deliver to the receiver; returns bytes or -1 */
+  virtual int SendMsg(const Message& msg) = 0;
+
+  PostOffice* po_;
+  Node my_node_;
+  std::atomic<bool> ready_{false};
+  std::atomic<int> timestamp_{0};
+  std::atomic<uint64_t> send_bytes_{0};
+  std::atomic<uint64_t> receive_bytes_{0};
+
+  friend class PostOffice;
+};
+
+}  // namespace ps

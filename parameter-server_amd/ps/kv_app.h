@@ -1,0 +1,591 @@
+// ps/kv_app.h — KVWorker / KVServer / KVServerDefaultHandle: the reference's
+// KV app surface (src/ps/KVApp.h:27-458) over the MI355X data path.
+//
+// What runs where
+//   worker  Push/Pull/PushPull build one request; the slicer cuts it by the
+//           servers' key ranges — with std::lower_bound for host key arrays
+//           (as KVApp.h:515-574) and with the psg_slice HIP kernel for key
+//           arrays in HBM; one message per non-empty slice (frames zero-copy).
+//   server  KVServerDefaultHandle keeps the value store in HBM (psg_store,
+//           SORTED layout) and runs every request as the psg_store_handle
+//           kernel.  Host frames are staged into HBM first; HBM frames (a
+//           worker that holds its keys / values on a GPU) are read in place,
+//           over xGMI when the worker's GPU is another one.
+//   merge   Pull replies are concatenated in key order: memcpy for host
+//           replies (KVApp.h:713-720), the psg_merge kernel for HBM replies.
+// Custom request handles registered with SetRequestHandle see host frames
+// (HBM frames are copied to host first), exactly like the reference; a handle
+// that can consume HBM frames registers with SetDeviceRequestHandle.
+#pragma once
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <type_traits>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "internal/PostOffice.h"
+#include "internal/customer.h"
+#include "internal/device.h"
+#include "ps/base.h"
+#include "ps/range.h"
+#include "ps/simple_app.h"
+#include "ps/svector.h"
+
+namespace ps {
+
+/* keys (unique, ascending), vals, optional per-key value lengths (KVApp.h:27-37) */
+template <typename Value>
+struct KVPairs {
+  SVector<Key> keys;
+  SVector<Value> vals;
+  SVector<int> lens;
+  int priority = 0;
+};
+
+/* meta of one request (KVApp.h:42-57) */
+struct KVMeta {
+  int cmd;
+  bool push;
+  bool pull;
+  int sender;
+  int timestamp;
+  int customer_id;
+};
+
+namespace detail {
+template <typename T>
+int DeviceOf(const std::vector<T>*) { return -1; }
+template <typename T>
+int DeviceOf(const SVector<T>* v) { return v->device(); }
+
+/* host copy of an HBM array (no-op for host arrays) */
+template <typename T>
+SVector<T> ToHost(const SVector<T>& v) {
+  if (!v.on_device() || v.empty()) return v;
+  SVector<T> h(v.size());
+  device::CopySync(h.data(), v.data(), v.size() * sizeof(T), 1);
+  return h;
+}
+/* HBM copy of a host array on GPU dev (no-op for HBM arrays) */
+template <typename T>
+SVector<T> ToDevice(const SVector<T>& v, int dev) {
+  if (v.on_device() || v.empty()) return v;
+  SVector<T> d = SVector<T>::OnDevice(v.size(), dev);
+  device::CopySync(d.data(), v.data(), v.size() * sizeof(T), 0);
+  return d;
+}
+}  // namespace detail
+
+template <typename Value>
+struct KVServerDefaultHandle;
+
+template <typename Value>
+class KVWorker : public SimpleApp {
+ public:
+  using Data = KVPairs<Value>;
+  using Callback = std::function<void()>;
+  using SlicedKVs = std::vector<std::pair<bool, Data>>;
+  using Slicer = std::function<void(Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced)>;
+
+  KVWorker(int app_id, int customer_id) : SimpleApp() {
+    slicer_ = [this](Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced) {
+      DefaultSlicer(send, ranges, sliced);
+    };
+    customer_ = new Customer(app_id, customer_id, [this](const Message& m) { OnReceive(m); });
+  }
+  ~KVWorker() override {
+    delete customer_;
+    customer_ = nullptr;
+  }
+
+  /* KVApp.h:112-122: the vectors are copied into SVectors */
+  int Push(const std::vector<Key>& keys, const std::vector<Value>& vals,
+           const std::vector<int>& lens = {}, int cmd = 0, const Callback& cb = nullptr,
+           int priority = 0) {
+    return ZPush(SVector<Key>(keys), SVector<Value>(vals), SVector<int>(lens), cmd, cb, priority);
+  }
+
+  /* KVApp.h:148-162 */
+  int Pull(const std::vector<Key>& keys, std::vector<Value>* vals, std::vector<int>* lens = nullptr,
+           int cmd = 0, const Callback& cb = nullptr, int priority = 0) {
+    SVector<Key> skeys(keys);
+    int ts = AddPullCB(skeys, vals, lens, cmd, cb);
+    Data kvs;
+    kvs.keys = skeys;
+    kvs.priority = priority;
+    Send(ts, false, true, cmd, kvs);
+    return ts;
+  }
+
+  /* KVApp.h:188-213 */
+  int PushPull(const std::vector<Key>& keys, const std::vector<Value>& vals, std::vector<Value>* outs,
+               std::vector<int>* lens = nullptr, int cmd = 0, const Callback& cb = nullptr,
+               int priority = 0) {
+    CHECK_NOTNULL(outs);
+    if (outs->empty())
+      outs->resize(vals.size());
+    else
+      CHECK_EQ(vals.size(), outs->size());
+    SVector<Key> skeys(keys);
+    SVector<Value> svals(vals);
+    auto souts = new SVector<Value>(outs->data(), outs->size());
+    SVector<int>* slens = lens ? new SVector<int>(lens->data(), lens->size()) : nullptr;
+    return ZPushPull(skeys, svals, souts, slens, cmd,
+                     [souts, slens, cb]() {
+                       delete souts;
+                       delete slens;
+                       if (cb) cb();
+                     },
+                     priority);
+  }
+
+  void Wait(int timestamp) override { customer_->WaitRequest(timestamp); }
+
+  /* zero-copy forms (KVApp.h:234-291); SVectors may live in HBM */
+  int ZPush(const SVector<Key>& keys, const SVector<Value>& vals, const SVector<int>& lens = {},
+            int cmd = 0, const Callback& cb = nullptr, int priority = 0) {
+    int ts = customer_->NewRequest(kServerGroup);
+    AddCallback(ts, cb);
+    Data kvs;
+    kvs.keys = keys;
+    kvs.vals = vals;
+    kvs.lens = lens;
+    kvs.priority = priority;
+    Send(ts, true, false, cmd, kvs);
+    return ts;
+  }
+  int ZPull(const SVector<Key>& keys, SVector<Value>* vals, SVector<int>* lens = nullptr, int cmd = 0,
+            const Callback& cb = nullptr, int priority = 0) {
+    int ts = AddPullCB(keys, vals, lens, cmd, cb);
+    Data kvs;
+    kvs.keys = keys;
+    kvs.priority = priority;
+    Send(ts, false, true, cmd, kvs);
+    return ts;
+  }
+  int ZPushPull(const SVector<Key>& keys, const SVector<Value>& vals, SVector<Value>* outs,
+                SVector<int>* lens = nullptr, int cmd = 0, const Callback& cb = nullptr,
+                int priority = 0) {
+    int ts = AddPullCB(keys, outs, lens, cmd, cb);
+    Data kvs;
+    kvs.keys = keys;
+    kvs.vals = vals;
+    kvs.priority = priority;
+    if (lens) kvs.lens = *lens;  // the reference forwards the output lens (KVApp.h:287-288)
+    Send(ts, true, true, cmd, kvs);
+    return ts;
+  }
+
+  void set_slicer(const Slicer& slicer) {
+    CHECK(static_cast<bool>(slicer));
+    slicer_ = slicer;
+  }
+
+ private:
+  struct Reply {
+    Data kv;
+    int sender;
+  };
+
+  void AddCallback(int timestamp, const Callback& cb) {
+    if (!cb) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    callbacks_[timestamp] = cb;
+  }
+  void RunCallback(int timestamp);
+  void Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs);
+  void OnReceive(const Message& msg) override;
+  void DefaultSlicer(Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced);
+  template <typename C, typename D>
+  int AddPullCB(const SVector<Key>& keys, C* vals, D* lens, int cmd, const Callback& cb);
+  template <typename C, typename D>
+  void MergePull(const SVector<Key>& keys, std::vector<Reply>& kvs, C* vals, D* lens);
+
+  std::unordered_map<int, std::vector<Reply>> recv_kvs_;
+  std::unordered_map<int, Callback> callbacks_;
+  std::mutex mu_;
+  Slicer slicer_;
+};
+
+template <typename Value>
+class KVServer : public SimpleApp {
+ public:
+  using ReqHandle = std::function<void(const KVMeta& req_meta, const KVPairs<Value>& req_data, KVServer* server)>;
+
+  explicit KVServer(int app_id) : SimpleApp() {
+    customer_ = new Customer(app_id, app_id, [this](const Message& m) { OnReceive(m); });
+  }
+  ~KVServer() override {
+    delete customer_;
+    customer_ = nullptr;
+  }
+
+  /* a host handle: sees host frames (KVApp.h:405-408) */
+  void SetRequestHandle(const ReqHandle& request_handle) {
+    CHECK(static_cast<bool>(request_handle)) << "invalid request handle";
+    request_handle_ = request_handle;
+    device_frames_ = false;
+  }
+  /* the default handle keeps its store in HBM and takes frames where they are */
+  void SetRequestHandle(const KVServerDefaultHandle<Value>& h) {
+    request_handle_ = h;
+    device_frames_ = true;
+  }
+  /* a handle that consumes HBM frames itself */
+  void SetDeviceRequestHandle(const ReqHandle& request_handle) {
+    CHECK(static_cast<bool>(request_handle)) << "invalid request handle";
+    request_handle_ = request_handle;
+    device_frames_ = true;
+  }
+
+  /* reply to a request (KVApp.h:491-513); frames may be host or HBM */
+  void Response(const KVMeta& req, const KVPairs<Value>& res = KVPairs<Value>());
+
+ private:
+  void OnReceive(const Message& msg) override;
+  ReqHandle request_handle_;
+  bool device_frames_ = false;
+};
+
+/* The default handle (KVApp.h:433-458): `store[key] += val` for a push,
+ * `res.vals[i] = store[key]` (post-update) for a pull, absent keys inserted
+ * with 0 — with the store in HBM (psg_store, SORTED) and the loop as one HIP
+ * kernel per request.  One value per key (the reference's CHECK at :441). */
+template <typename Value>
+struct KVServerDefaultHandle {
+  struct State {
+    psg_store* store = nullptr;
+    ~State() {
+      if (store) psg_store_destroy(store);
+    }
+  };
+  std::shared_ptr<State> state = std::make_shared<State>();
+
+  void operator()(const KVMeta& req_meta, const KVPairs<Value>& req_data, KVServer<Value>* server) {
+    const size_t n = req_data.keys.size();
+    KVPairs<Value> res;
+    if (req_meta.push) CHECK_EQ(n, req_data.vals.size());
+    const int dev = PostOffice::Get()->device();
+    CHECK_GE(dev, 0) << "KVServerDefaultHandle: the value store lives in HBM and this node has no GPU";
+    constexpr int dt = device::DType<Value>();
+    CHECK_GE(dt, 0) << "KVServerDefaultHandle: value type not supported by the HBM store";
+    if (!state->store)
+      device::Check(psg_store_create(PSG_STORE_SORTED, dt, 0, kMaxKey, 0, &state->store), "psg_store_create");
+    const bool on_dev = req_data.keys.on_device();
+    const int flags = (req_meta.push ? PSG_PUSH : 0) | (req_meta.pull ? PSG_PULL : 0);
+    SVector<Value> dout;
+    if (n && flags) {
+      SVector<Key> dkeys = detail::ToDevice(req_data.keys, dev);
+      SVector<Value> dvals;
+      if (req_meta.push) dvals = detail::ToDevice(req_data.vals, dev);
+      if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
+      psg_stream s = device::ThreadStream();
+      device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
+                    "psg_store_handle");
+      device::Check(psg_stream_sync(s), "psg_stream_sync");
+    }
+    if (req_meta.pull) {
+      res.keys = req_data.keys;
+      res.vals = on_dev ? dout : detail::ToHost(dout);
+    }
+    server->Response(req_meta, res);
+  }
+
+  psg_store* store() const { return state->store; }
+  /* (key, value) pairs in key order, copied to host */
+  void Dump(std::vector<Key>* keys, std::vector<Value>* vals) const {
+    keys->clear();
+    vals->clear();
+    if (!state->store) return;
+    psg_store_info info;
+    device::Check(psg_store_get_info(state->store, &info), "psg_store_get_info");
+    keys->resize(info.size);
+    vals->resize(info.size);
+    device::Check(psg_store_dump(state->store, keys->data(), vals->data()), "psg_store_dump");
+  }
+};
+
+// ============================================================================
+// KVServer
+
+template <typename Value>
+void KVServer<Value>::OnReceive(const Message& msg) {
+  if (msg.meta.simple_app) {
+    SimpleApp::OnReceive(msg);
+    return;
+  }
+  KVMeta meta;
+  meta.cmd = msg.meta.head;
+  meta.push = msg.meta.push;
+  meta.pull = msg.meta.pull;
+  meta.sender = msg.meta.sender;
+  meta.timestamp = msg.meta.timestamp;
+  meta.customer_id = msg.meta.customer_id;
+  KVPairs<Value> data;
+  const size_t n = msg.data.size();
+  if (n) {
+    CHECK_GE(n, (size_t)2);
+    data.keys = msg.data[0];
+    data.vals = msg.data[1];
+    if (n > 2) {
+      CHECK_EQ(n, (size_t)3);
+      data.lens = msg.data[2];
+      CHECK_EQ(data.lens.size(), data.keys.size());
+    }
+    if (!device_frames_) {
+      data.keys = detail::ToHost(data.keys);
+      data.vals = detail::ToHost(data.vals);
+      data.lens = detail::ToHost(data.lens);
+    }
+  }
+  CHECK(static_cast<bool>(request_handle_));
+  request_handle_(meta, data, this);
+}
+
+template <typename Value>
+void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
+  Message msg;
+  msg.meta.app_id = customer_->app_id();
+  msg.meta.customer_id = req.customer_id;
+  msg.meta.request = false;
+  msg.meta.push = req.push;
+  msg.meta.pull = req.pull;
+  msg.meta.head = req.cmd;
+  msg.meta.timestamp = req.timestamp;
+  msg.meta.receiver = req.sender;
+  if (res.keys.size()) {
+    msg.AddData(res.keys);
+    msg.AddData(res.vals);
+    if (res.lens.size()) msg.AddData(res.lens);
+  }
+  PostOffice::Get()->van()->Send(msg);
+}
+
+// ============================================================================
+// KVWorker
+
+template <typename Value>
+void KVWorker<Value>::DefaultSlicer(Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced) {
+  const size_t n = ranges.size();
+  sliced->resize(n);
+  std::vector<uint64_t> pos(n + 1, 0), vpos(n + 1, 0);
+  const size_t nkeys = send.keys.size();
+  if (send.keys.on_device()) {
+    if (send.lens.size()) {
+      CHECK_EQ(send.keys.size(), send.lens.size());
+      CHECK(send.lens.on_device()) << "device keys need device lens";
+    }
+    device::SliceKeys(send.keys.data(), nkeys, send.lens.size() ? send.lens.data() : nullptr,
+                      send.vals.size(), ranges, &pos, &vpos);
+  } else {
+    const Key* begin = send.keys.begin();
+    const Key* end = send.keys.end();
+    for (size_t i = 0; i < n; ++i) {
+      if (i == 0) {
+        pos[0] = std::lower_bound(begin, end, ranges[0].begin) - begin;
+        begin += pos[0];
+      } else {
+        CHECK_EQ(ranges[i - 1].end, ranges[i].begin);
+      }
+      size_t len = std::lower_bound(begin, end, ranges[i].end) - begin;
+      begin += len;
+      pos[i + 1] = pos[i] + len;
+    }
+    CHECK_EQ(pos[n], nkeys);
+    if (nkeys) {
+      if (send.lens.empty()) {
+        const size_t k = send.vals.size() / nkeys;
+        CHECK_EQ(k * nkeys, send.vals.size());
+        for (size_t i = 0; i <= n; ++i) vpos[i] = pos[i] * k;
+      } else {
+        CHECK_EQ(nkeys, send.lens.size());
+        SVector<int> hl = detail::ToHost(send.lens);
+        uint64_t acc = 0;
+        for (size_t i = 0; i < n; ++i) {
+          vpos[i] = acc;
+          for (size_t j = pos[i]; j < pos[i + 1]; ++j) acc += hl[j];
+        }
+        vpos[n] = acc;
+      }
+    }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    auto& s = sliced->at(i);
+    s.first = pos[i + 1] != pos[i];
+    if (!s.first) continue;
+    s.second.keys = send.keys.Slice(pos[i], pos[i + 1]);
+    s.second.vals = send.vals.Slice(vpos[i], vpos[i + 1]);
+    if (send.lens.size()) s.second.lens = send.lens.Slice(pos[i], pos[i + 1]);
+  }
+}
+
+template <typename Value>
+void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs) {
+  SlicedKVs sliced;
+  slicer_(const_cast<Data&>(kvs), PostOffice::Get()->GetServerRanges(), &sliced);
+  int skipped = 0;
+  for (auto& s : sliced)
+    if (!s.first) ++skipped;
+  customer_->AddResponse(timestamp, skipped);
+  if ((size_t)skipped == sliced.size()) RunCallback(timestamp);
+  for (size_t i = 0; i < sliced.size(); ++i) {
+    const auto& s = sliced[i];
+    if (!s.first) continue;
+    Message msg;
+    msg.meta.app_id = customer_->app_id();
+    msg.meta.customer_id = customer_->customer_id();
+    msg.meta.request = true;
+    msg.meta.push = push;
+    msg.meta.pull = pull;
+    msg.meta.head = cmd;
+    msg.meta.timestamp = timestamp;
+    msg.meta.receiver = PostOffice::ServerRankToID((int)i);
+    msg.meta.priority = kvs.priority;
+    const auto& kv = s.second;
+    if (kv.keys.size()) {
+      msg.AddData(kv.keys);
+      msg.AddData(kv.vals);
+      if (kv.lens.size()) msg.AddData(kv.lens);
+    }
+    PostOffice::Get()->van()->Send(msg);
+  }
+}
+
+template <typename Value>
+void KVWorker<Value>::OnReceive(const Message& msg) {
+  if (msg.meta.simple_app) {
+    SimpleApp::OnReceive(msg);
+    return;
+  }
+  const int ts = msg.meta.timestamp;
+  if (msg.meta.pull) {
+    CHECK_GE(msg.data.size(), (size_t)2);
+    Reply r;
+    r.kv.keys = msg.data[0];
+    r.kv.vals = msg.data[1];
+    if (msg.data.size() > 2) r.kv.lens = msg.data[2];
+    r.sender = msg.meta.sender;
+    std::lock_guard<std::mutex> lk(mu_);
+    recv_kvs_[ts].push_back(std::move(r));
+  }
+  // the tracker is bumped after this handle returns (Customer.cpp:58-67)
+  if (customer_->GetResponse(ts) == PostOffice::Get()->num_servers() - 1) RunCallback(ts);
+}
+
+template <typename Value>
+void KVWorker<Value>::RunCallback(int timestamp) {
+  Callback cb;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = callbacks_.find(timestamp);
+    if (it == callbacks_.end()) return;
+    cb = std::move(it->second);
+    callbacks_.erase(it);
+  }
+  CHECK(static_cast<bool>(cb));
+  cb();
+}
+
+template <typename Value>
+template <typename C, typename D>
+int KVWorker<Value>::AddPullCB(const SVector<Key>& keys, C* vals, D* lens, int cmd, const Callback& cb) {
+  (void)cmd;
+  int ts = customer_->NewRequest(kServerGroup);
+  AddCallback(ts, [this, ts, keys, vals, lens, cb]() mutable {
+    std::vector<Reply> kvs;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = recv_kvs_.find(ts);
+      if (it != recv_kvs_.end()) {
+        kvs.swap(it->second);
+        recv_kvs_.erase(it);
+      }
+    }
+    MergePull(keys, kvs, vals, lens);
+    if (cb) cb();
+  });
+  return ts;
+}
+
+template <typename Value>
+template <typename C, typename D>
+void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kvs, C* vals, D* lens) {
+  size_t total_key = 0, total_val = 0;
+  int ndev = 0;
+  for (const auto& r : kvs) {
+    const auto& s = r.kv;
+    if (!s.keys.on_device() && !keys.on_device() && s.keys.size()) {
+      Range range = FindRange(keys, s.keys.front(), s.keys.back() + 1);
+      CHECK_EQ(range.size(), s.keys.size()) << "unmatched keys size from one server";
+    }
+    if (lens) CHECK_EQ(s.lens.size(), s.keys.size());
+    total_key += s.keys.size();
+    total_val += s.vals.size();
+    ndev += s.vals.on_device() ? 1 : 0;
+  }
+  CHECK_EQ(total_key, keys.size()) << "lost some servers?";
+  CHECK(ndev == 0 || ndev == (int)kvs.size()) << "pull replies mix host and HBM frames";
+  // order the replies by their first key (KVApp.h:694-696); replies whose keys
+  // are in HBM are ordered by server rank, which the default ranges make the same
+  if (!keys.on_device()) {
+    std::sort(kvs.begin(), kvs.end(), [](const Reply& a, const Reply& b) {
+      return a.kv.keys.front() < b.kv.keys.front();
+    });
+  } else {
+    std::sort(kvs.begin(), kvs.end(), [](const Reply& a, const Reply& b) { return a.sender < b.sender; });
+  }
+  CHECK_NOTNULL(vals);
+  const int out_dev = detail::DeviceOf(vals);
+  if (vals->empty()) {
+    CHECK_LT(out_dev, 0) << "an HBM pull output must be sized by the caller";
+    vals->resize(total_val);
+  } else {
+    CHECK_EQ(vals->size(), total_val);
+  }
+  if (ndev == 0 && out_dev < 0) {
+    Value* p = vals->data();
+    for (const auto& r : kvs) {
+      if (r.kv.vals.size()) std::memcpy(p, r.kv.vals.data(), r.kv.vals.size() * sizeof(Value));
+      p += r.kv.vals.size();
+    }
+  } else if (total_val) {
+    std::vector<psg_segment> segs;
+    std::vector<SVector<Value>> staged;  // host replies going to an HBM output
+    const int my_dev = PostOffice::Get()->device();
+    for (size_t j = 0; j < kvs.size(); ++j) {
+      const SVector<Value>& v = kvs[j].kv.vals;
+      const Value* src = v.data();
+      if (!v.on_device() && v.size()) {
+        staged.push_back(detail::ToDevice(v, out_dev >= 0 ? out_dev : my_dev));
+        src = staged.back().data();
+      }
+      segs.push_back(psg_segment{src, v.size(), (uint64_t)j});  // j: already in order
+    }
+    if (out_dev >= 0) {
+      device::Merge(&segs, sizeof(Value), vals->data(), total_val);
+    } else {
+      SVector<Value> tmp = SVector<Value>::OnDevice(total_val, my_dev);
+      device::Merge(&segs, sizeof(Value), tmp.data(), total_val);
+      device::CopySync(vals->data(), tmp.data(), total_val * sizeof(Value), 1);
+    }
+  }
+  if (lens) {
+    CHECK_LT(detail::DeviceOf(lens), 0) << "pull lens are returned in host memory";
+    if (lens->empty())
+      lens->resize(keys.size());
+    else
+      CHECK_EQ(lens->size(), keys.size());
+    int* p = lens->data();
+    for (const auto& r : kvs) {
+      SVector<int> hl = detail::ToHost(r.kv.lens);
+      if (hl.size()) std::memcpy(p, hl.data(), hl.size() * sizeof(int));
+      p += hl.size();
+    }
+  }
+}
+
+}  // namespace ps

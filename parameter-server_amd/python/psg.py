@@ -34,7 +34,7 @@ _ESIZE = {F32: 4, F64: 8, F16: 2, BF16: 2}
 # every symbol include/psg.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "psg_abi_version", "psg_last_error", "psg_device_count", "psg_set_device",
-    "psg_get_device", "psg_device_sync", "psg_malloc", "psg_free", "psg_host_alloc",
+    "psg_get_device", "psg_device_sync", "psg_enable_peer_access", "psg_malloc", "psg_free", "psg_host_alloc",
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
     "psg_memset", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
     "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
             "psg_abi_version": ([], i32), "psg_last_error": ([], C.c_char_p),
             "psg_device_count": ([C.POINTER(i32)], i32), "psg_set_device": ([i32], i32),
             "psg_get_device": ([C.POINTER(i32)], i32), "psg_device_sync": ([], i32),
+            "psg_enable_peer_access": ([i32, i32], i32),
             "psg_malloc": ([C.POINTER(vp), C.c_size_t], i32), "psg_free": ([vp], i32),
             "psg_host_alloc": ([C.POINTER(vp), C.c_size_t], i32), "psg_host_free": ([vp], i32),
             "psg_host_register": ([vp, C.c_size_t], i32), "psg_host_unregister": ([vp], i32),

@@ -1,0 +1,137 @@
+// device.cc — GPU plumbing of the host runtime, all through the psg C-ABI.
+#include "internal/device.h"
+
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "ps/log.h"
+#include "ps/svector.h"
+
+namespace ps {
+namespace device {
+
+void Check(int rc, const char* what) {
+  if (rc != PSG_OK) ps_log::LogMessageFatal(__FILE__, __LINE__).stream() << what << ": " << psg_last_error();
+}
+
+int Count() {
+  static int n = [] {
+    int c = 0;
+    if (psg_device_count(&c) != PSG_OK) c = 0;
+    return c;
+  }();
+  return n;
+}
+
+void Use(int dev) {
+  if (dev < 0) return;
+  Check(psg_set_device(dev), "psg_set_device");
+}
+
+namespace {
+// Streams live as long as the process: destroying them from thread_local
+// destructors could run after the HIP runtime has been torn down.
+struct ThreadStreams {
+  std::map<int, psg_stream> by_dev;
+};
+thread_local ThreadStreams t_streams;
+
+// Caching HBM pool: freed blocks are kept per (device, rounded size) and
+// reused, so per-request reply / staging buffers cost no hipMalloc after
+// warm-up.  Sizes round up to 64 KiB granules (or the next power of two
+// above 64 MiB).
+struct Pool {
+  std::mutex mu;
+  std::map<std::pair<int, size_t>, std::vector<void*>> free;
+  static size_t Round(size_t b) {
+    if (b <= (64u << 20)) return (b + 65535) & ~size_t(65535);
+    size_t r = size_t(64) << 20;
+    while (r < b) r <<= 1;
+    return r;
+  }
+};
+Pool& GlobalPool() {
+  static Pool* p = new Pool();  // never destroyed: blocks may outlive static teardown
+  return *p;
+}
+}  // namespace
+
+psg_stream ThreadStream() {
+  int dev = 0;
+  Check(psg_get_device(&dev), "psg_get_device");
+  auto it = t_streams.by_dev.find(dev);
+  if (it != t_streams.by_dev.end()) return it->second;
+  psg_stream s = nullptr;
+  Check(psg_stream_create(&s), "psg_stream_create");
+  t_streams.by_dev[dev] = s;
+  return s;
+}
+
+std::shared_ptr<void> Alloc(size_t bytes, int dev) {
+  CHECK_GE(dev, 0) << "device allocation without a GPU";
+  if (bytes == 0) return nullptr;
+  Pool& pool = GlobalPool();
+  const size_t rb = Pool::Round(bytes);
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    auto& fl = pool.free[{dev, rb}];
+    if (!fl.empty()) {
+      p = fl.back();
+      fl.pop_back();
+    }
+  }
+  if (!p) {
+    int cur = 0;
+    Check(psg_get_device(&cur), "psg_get_device");
+    if (cur != dev) Use(dev);
+    int rc = psg_malloc(&p, rb);
+    if (cur != dev) Use(cur);
+    Check(rc, "psg_malloc");
+  }
+  return std::shared_ptr<void>(p, [dev, rb](void* q) {
+    Pool& pl = GlobalPool();
+    std::lock_guard<std::mutex> lk(pl.mu);
+    pl.free[{dev, rb}].push_back(q);
+  });
+}
+
+void EnableAllPeerAccess() {
+  const int n = Count();
+  for (int a = 0; a < n; ++a)
+    for (int b = 0; b < n; ++b)
+      if (a != b) Check(psg_enable_peer_access(a, b), "psg_enable_peer_access");
+}
+
+void CopySync(void* dst, const void* src, size_t bytes, int kind) {
+  if (!bytes) return;
+  psg_stream s = ThreadStream();
+  Check(psg_memcpy(dst, src, bytes, kind, s), "psg_memcpy");
+  Check(psg_stream_sync(s), "psg_stream_sync");
+}
+
+void SliceKeys(const uint64_t* keys, size_t n, const int* lens, size_t num_vals,
+               const std::vector<Range>& ranges, std::vector<uint64_t>* key_pos,
+               std::vector<uint64_t>* val_pos) {
+  const size_t ns = ranges.size();
+  std::vector<uint64_t> b(ns), e(ns);
+  for (size_t i = 0; i < ns; ++i) {
+    b[i] = ranges[i].begin;
+    e[i] = ranges[i].end;
+  }
+  key_pos->assign(ns + 1, 0);
+  val_pos->assign(ns + 1, 0);
+  Check(psg_slice(keys, n, lens, num_vals, (int)ns, b.data(), e.data(), key_pos->data(), val_pos->data(),
+                  ThreadStream()),
+        "psg_slice");
+}
+
+void Merge(std::vector<psg_segment>* segs, int elem_size, void* dst, uint64_t dst_count) {
+  psg_stream s = ThreadStream();
+  Check(psg_merge(segs->data(), (int)segs->size(), elem_size, dst, dst_count, s), "psg_merge");
+  Check(psg_stream_sync(s), "psg_stream_sync");
+}
+
+}  // namespace device
+}  // namespace ps

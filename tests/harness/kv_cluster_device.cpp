@@ -1,0 +1,86 @@
+// kv_cluster_device.cpp — the KV API end to end on the GPU data path.
+//
+// Workers hold keys and values either in HBM (ZPush / ZPull on device
+// SVectors: device slicer, frames read in place by the server kernels, pull
+// replies merged by psg_merge) or in host std::vectors (Push / Pull: frames
+// staged into HBM by the server handle, replies copied back).  The servers run
+// KVServerDefaultHandle<float> (HBM store).  Checks the test_kv_app.cpp
+// expectations (50 pushes -> 50 * vals, 50 push-pulls -> 100 * vals) and
+// prints one JSON line of timings per worker:
+//   {"rank":r,"n":N,"device_push_ms":..,"device_pull_ms":..,"host_push_ms":..,"host_pull_ms":..}
+// usage: kv_cluster_device [-ns S] [-nw W] [num_keys] [repeat]
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+#include "internal/device.h"
+#include "ps/ps.h"
+
+using namespace ps;
+using clk = std::chrono::steady_clock;
+
+static double ms_since(clk::time_point t0) {
+  return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+}
+
+int main(int argc, char* argv[]) {
+  Start(0, argc, argv);
+  if (IsServer()) {
+    auto server = new KVServer<float>(0);
+    server->SetRequestHandle(KVServerDefaultHandle<float>());
+    RegisterExitCallback([server]() { delete server; });
+  }
+  if (IsWorker()) {
+    const long num = argc > 4 ? std::atol(argv[4]) : 1000000;
+    const int repeat = argc > 5 ? std::atoi(argv[5]) : 50;
+    const int rank = MyRank();
+    const int dev = PostOffice::Get()->device();
+    KVWorker<float> kv(0, 0);
+    psg_stream s = device::ThreadStream();
+
+    // ---- HBM-resident keys / values (the device-resident data path)
+    auto dkeys = SVector<Key>::OnDevice(num, dev);
+    auto dvals = SVector<float>::OnDevice(num, dev);
+    device::Check(psg_fill_keys_arith(dkeys.data(), num, rank, kMaxKey / num, s), "fill keys");
+    device::Check(psg_fill_synth(dvals.data(), num, PSG_F32, 7 + rank, 0, 0.0, 1000.0, s), "fill vals");
+    device::Check(psg_stream_sync(s), "sync");
+    std::vector<float> hvals(num);
+    device::CopySync(hvals.data(), dvals.data(), num * sizeof(float), 1);
+
+    auto t0 = clk::now();
+    for (int r = 0; r < repeat; ++r) kv.Wait(kv.ZPush(dkeys, dvals));
+    double dpush = ms_since(t0) / repeat;
+    auto dout = SVector<float>::OnDevice(num, dev);
+    t0 = clk::now();
+    kv.Wait(kv.ZPull(dkeys, &dout));
+    double dpull = ms_since(t0);
+    std::vector<float> got(num);
+    device::CopySync(got.data(), dout.data(), num * sizeof(float), 1);
+    for (long i = 0; i < num; ++i) CHECK_EQ(got[i], hvals[i] * repeat) << "device path, i=" << i;
+    for (int r = 0; r < repeat; ++r) kv.Wait(kv.ZPushPull(dkeys, dvals, &dout));
+    device::CopySync(got.data(), dout.data(), num * sizeof(float), 1);
+    for (long i = 0; i < num; ++i) CHECK_EQ(got[i], hvals[i] * 2 * repeat) << "device push-pull, i=" << i;
+
+    // ---- host std::vector keys / values (the reference's calling convention)
+    std::vector<Key> hkeys(num);
+    for (long i = 0; i < num; ++i) hkeys[i] = kMaxKey / num * i + rank + 1;  // fresh keys
+    t0 = clk::now();
+    for (int r = 0; r < repeat; ++r) kv.Wait(kv.Push(hkeys, hvals));
+    double hpush = ms_since(t0) / repeat;
+    std::vector<float> rets;
+    t0 = clk::now();
+    kv.Wait(kv.Pull(hkeys, &rets));
+    double hpull = ms_since(t0);
+    for (long i = 0; i < num; ++i) CHECK_EQ(rets[i], hvals[i] * repeat) << "host path, i=" << i;
+    std::vector<float> outs;
+    for (int r = 0; r < repeat; ++r) kv.Wait(kv.PushPull(hkeys, hvals, &outs));
+    for (long i = 0; i < num; ++i) CHECK_EQ(outs[i], hvals[i] * 2 * repeat) << "host push-pull, i=" << i;
+
+    std::printf("{\"rank\": %d, \"n\": %ld, \"servers\": %d, \"device_push_ms\": %.4f, "
+                "\"device_pull_ms\": %.4f, \"host_push_ms\": %.4f, \"host_pull_ms\": %.4f}\n",
+                rank, num, NumServers(), dpush, dpull, hpush, hpull);
+    std::fflush(stdout);
+  }
+  Finalize(0, true);
+  return 0;
+}

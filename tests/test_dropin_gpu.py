@@ -1,0 +1,76 @@
+"""The reference's own harnesses, compiled unmodified against this runtime,
+run on the MI355X: KVServerDefaultHandle<float> keeps its store in HBM and
+answers every request with the psg kernels.
+
+The binaries are built in the build container from /root/reference/tests
+(`make -C parameter-server_amd dropin`) and travel to the GPU box as build
+products; the reference sources never do.  test_kv_app.cpp and
+test_kv_app_multi_workers.cpp CHECK their known answers themselves (a failed
+CHECK aborts the job, non-zero exit).
+"""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DROPIN = os.path.join(ROOT, "tests", "_dropin")
+BIN = os.path.join(ROOT, "tests", "_bin")
+
+
+def run(path, *args, timeout=300):
+    return subprocess.run([path, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+
+
+def _need(path):
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not built")
+
+
+@pytest.mark.parametrize("ns,nw", [(1, 1), (2, 1), (4, 2)])
+def test_reference_test_kv_app(ns, nw):
+    exe = os.path.join(DROPIN, "test_kv_app")
+    _need(exe)
+    r = run(exe, "-ns", ns, "-nw", nw)
+    assert r.returncode == 0, r.stderr[-3000:]
+    errs = re.findall(r"got error value: ([\d.eE+-]+), ([\d.eE+-]+)", r.stdout)
+    assert len(errs) == nw and all(float(a) == 0 and float(b) == 0 for a, b in errs), r.stdout
+
+
+def test_reference_multi_workers():
+    exe = os.path.join(DROPIN, "test_kv_app_multi_workers")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 1)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("got error value: 0, 0") == 2, r.stdout
+
+
+def test_reference_test_my_runs():
+    # the reference comments its checks out (test_my.cpp:76-77); the run must complete
+    exe = os.path.join(DROPIN, "test_my")
+    _need(exe)
+    r = run(exe, "-ns", 1, "-nw", 1)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("got error value") == 3
+
+
+def test_reference_benchmark_runs():
+    exe = os.path.join(DROPIN, "test_kv_app_benchmark")
+    _need(exe)
+    r = run(exe, "-ns", 1, "-nw", 1)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Push average time" in r.stdout and "Pull average time" in r.stdout
+
+
+@pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
+def test_device_frames_end_to_end(ns, nw):
+    exe = os.path.join(BIN, "kv_cluster_device")
+    _need(exe)
+    r = run(exe, "-ns", ns, "-nw", nw, 200000, 20)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == nw
