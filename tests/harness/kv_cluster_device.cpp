@@ -63,7 +63,8 @@ int main(int argc, char* argv[]) {
 
     // ---- host std::vector keys / values (the reference's calling convention)
     std::vector<Key> hkeys(num);
-    for (long i = 0; i < num; ++i) hkeys[i] = kMaxKey / num * i + rank + 1;  // fresh keys
+    // fresh keys, disjoint from every worker's device-path keys (offset >= NumWorkers())
+    for (long i = 0; i < num; ++i) hkeys[i] = kMaxKey / num * i + NumWorkers() + rank;
     t0 = clk::now();
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.Push(hkeys, hvals));
     double hpush = ms_since(t0) / repeat;

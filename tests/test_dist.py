@@ -1,0 +1,119 @@
+"""The N > 1 data path of bench.py, rehearsed on CPU with world_size 2 (gloo).
+
+bench.run() is the same orchestration the GPU job runs (shards, warmup,
+barriers, max-over-ranks timing, the JSON line); only the backend differs:
+here a Push is torch.distributed.reduce_scatter_tensor + the shard accumulate
+and a Pull is all_gather_into_tensor — the collective pattern psg_comm_push /
+psg_comm_pull issue on RCCL.  The result is checked against the oracle
+replaying every worker's Push as a separate KVServerDefaultHandle request, in
+worker order, on real-valued data: the reduce-scatter sums in another order,
+so the bar is the north star's 1e-6 relative tolerance (plus an absolute floor
+for sums that cancel to ~0).
+"""
+import argparse
+import json
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REL_TOL = 1e-6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class CpuCollectiveBackend:
+    """bench.py backend whose Push/Pull run the RS + accumulate / AG pattern on gloo."""
+
+    def __init__(self, rank, world, dist):
+        import torch
+        self.torch, self.rank, self.world, self.dist = torch, rank, world, dist
+
+    def setup(self, L, seed):
+        import oracle
+        self.L, self.blk = L, L // self.world
+        self.vals = self.torch.from_numpy(oracle.synth(L, oracle.F32, seed + self.rank, 1, -1.0, 1.0))
+        self.store = self.torch.zeros(self.blk, dtype=self.torch.float32)
+        self.out = self.torch.zeros(L, dtype=self.torch.float32)
+        self.pushes = 0
+
+    def push(self):
+        scratch = self.torch.zeros(self.blk, dtype=self.torch.float32)
+        self.dist.reduce_scatter_tensor(scratch, self.vals)
+        self.store += scratch
+        self.pushes += 1
+
+    def pull(self):
+        self.dist.all_gather_into_tensor(self.out, self.store)
+
+    def new_event(self):
+        return [0.0]
+
+    def record(self, e):
+        import time
+        e[0] = time.perf_counter()
+
+    def elapsed(self, a, b):
+        return (b[0] - a[0]) * 1e3
+
+    def sync(self):
+        pass
+
+    def check(self, steps_done):
+        import oracle
+        self.pull()
+        got = self.out.numpy()
+        ok = True
+        for r in range(self.world):
+            st = oracle.Store(oracle.F32)
+            lo = r * self.blk
+            for _ in range(steps_done):
+                for w in range(self.world):
+                    v = oracle.synth(self.L, oracle.F32, self._seed + w, 1, -1.0, 1.0)[lo:lo + self.blk]
+                    st.handle(oracle.PUSH, None, v, self.blk, first_key=lo)
+            exp = st.handle(oracle.PULL, None, None, self.blk, first_key=lo)
+            g = got[lo:lo + self.blk]
+            ok &= bool(np.all(np.abs(g - exp) <= REL_TOL * np.abs(exp) + 1e-6 * steps_done * self.world))
+        return ok
+
+
+def _rank_main(rank, world, port, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "parameter-server_amd", "python")]
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    import bench
+    args = argparse.Namespace(keys=12288, seed=7, warmup=1, steps=3, check=1, no_cpu_baseline=True)
+    res = bench.run(CpuCollectiveBackend(rank, world, dist), args, rank, world, dist)
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_distributed_path_gloo(world):
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rank_main, args=(world, _free_port(), d), nprocs=world, join=True)
+        r0 = json.load(open(os.path.join(d, "r0.json")))
+        for r in range(1, world):
+            assert json.load(open(os.path.join(d, f"r{r}.json"))) is None  # only rank 0 prints
+    assert r0["n_gpus"] == world and r0["scaling"] == "weak"
+    assert r0["parity_check"] is True
+    assert r0["config"]["shard_keys"] * world == r0["config"]["keys_per_worker"]
+    # value = all workers' pushed + pulled floats / max-over-ranks time
+    exp = 2 * 4 * r0["config"]["keys_per_worker"] * world / (r0["ms_per_step"] * 1e-3) / 1e9
+    assert abs(r0["value"] - exp) <= 1e-3 * exp + 1e-3
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in r0
