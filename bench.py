@@ -1,19 +1,22 @@
 #!/usr/bin/env python3
 """Device-resident KV Push+Pull GB/s (float vals) — the BASELINE.json metric.
 
-One step = one worker Push of its dense float vector followed by one Pull of
-the same keys (tests/test_kv_app_benchmark.cpp:54-81 semantics, buffers already
-in HBM, keys implicit and consecutive):
+One step = one worker Push of its dense value vector followed by one Pull of the
+same keys (tests/test_kv_app_benchmark.cpp:54-81 semantics, buffers already in
+HBM, keys implicit and consecutive):
 
   N = 1   configs[1]: 1 server + 1 worker, L = 64 M floats.  Push is the
           KVServerDefaultHandle accumulate (src/ps/KVApp.h:446-454) as one
           streaming HIP kernel over the DENSE store; Pull is the read-back.
-  N > 1   configs[3] shape, one process per GPU, rank r = worker r + server
+  N > 1   configs[2] shape, one process per GPU, rank r = worker r + server
           shard r (L / N keys): Push = RCCL reduce-scatter + the accumulate
-          kernel, Pull = RCCL all-gather (psg_comm_push / psg_comm_pull).
+          kernel, Pull = RCCL all-gather (psg_comm_push / psg_comm_pull), or
+          the two pipelined over buckets (psg_comm_push_pull) — whichever a
+          short calibration in the warm-up finds faster on this node.
 
-value = (4 B * L pushed + 4 B * L pulled) * N / (max-over-ranks time per step)
-(weak scaling: every worker moves L floats each way at every N).
+value = (B * L pushed + B * L pulled) * N / (max-over-ranks time per step),
+B = bytes per value (weak scaling: every worker moves L values each way at
+every N).  `--workload dense-f16` runs configs[4] (f16 values, 1 B per worker).
 
 Prints ONE JSON line on rank 0.  Launch for N > 1:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -33,39 +36,52 @@ for _p in (os.path.join(ROOT, "parameter-server_amd", "python"), os.path.join(RO
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
-F32_BYTES = 4
-PUSH_BYTES_PER_ELEM = 12  # read vals + read store + write store
-PULL_BYTES_PER_ELEM = 8   # read store + write out
+PUSH_ACCESSES = 3      # read vals + read store + write store
+PULL_ACCESSES = 2      # read store + write out
+
+WORKLOADS = {
+    # name: (dtype name, value bytes, default values per worker, description)
+    "dense": ("f32", 4, 64 << 20, "configs[1]"),
+    "dense-f16": ("f16", 2, 1 << 30, "configs[4]"),
+}
 
 
 class GpuBackend:
     """The product path: psg C-ABI (HIP kernels + RCCL)."""
 
-    def __init__(self, rank: int, world: int, local_rank: int, dist=None):
+    def __init__(self, rank: int, world: int, local_rank: int, dist=None, dtype="f32"):
         import psg
         self.p = psg
         self.rank, self.world, self.dist = rank, world, dist
+        self.dt = {"f32": psg.F32, "f16": psg.F16}[dtype]
+        self.vb = {"f32": 4, "f16": 2}[dtype]
         psg.set_device(local_rank)
         self.stream = psg.Stream()
         self.comm = None
+        self.fused = False
+        self.nbuckets = 1
 
     def setup(self, L: int, seed: int):
         p = self.p
         blk = L // self.world
-        self.L, self.blk = L, blk
+        self.L, self.blk, self._seed = L, blk, seed
         lo = self.rank * blk
-        self.store = p.Store(p.DENSE, p.F32, lo, lo + blk, blk)
-        self.vals = p.DeviceBuffer(L * F32_BYTES)
-        self.vals.fill_synth(L, p.F32, seed + self.rank, 0, 0.0, 1000.0, self.stream)
-        self.out = p.DeviceBuffer(L * F32_BYTES)
+        self.store = p.Store(p.DENSE, self.dt, lo, lo + blk, blk)
+        self.vals = p.DeviceBuffer(L * self.vb)
+        # integer-valued 0..99 (f16 holds them and their sums exactly) / 0..999 (f32)
+        self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self._hi(), self.stream)
+        self.out = p.DeviceBuffer(L * self.vb)
         if self.world > 1:
             uid = [p.comm_id() if self.rank == 0 else None]
             self.dist.broadcast_object_list(uid, src=0)
             self.comm = p.Comm(uid[0], self.world, self.rank)
-            self.scratch = p.DeviceBuffer(blk * F32_BYTES)
-        self.ev = []
+            self.scratch = p.DeviceBuffer(blk * self.vb)
         self.sync()
 
+    def _hi(self):
+        return 1000.0 if self.dt == self.p.F32 else 8.0
+
+    # -- one phase at a time (N = 1, or the sequential RS / AG at N > 1)
     def push(self):
         if self.comm is None:
             self.store.handle(self.p.PUSH, None, self.vals, None, self.L, first_key=0,
@@ -80,6 +96,37 @@ class GpuBackend:
         else:
             self.comm.pull(self.store, self.out, self.L, self.stream)
 
+    # -- both, pipelined over buckets (N > 1)
+    def step(self):
+        self.comm.push_pull(self.store, self.vals, self.out, self.L, self.nbuckets, self.stream)
+
+    def calibrate(self, dist, iters=3):
+        """Pick sequential RS+AG (nbuckets 1) or a pipelined bucket count by timing
+        each a few times; the max over ranks decides, so every rank picks the same."""
+        if self.comm is None:
+            return
+        import torch
+        cands = [1, 4, 8, 16]
+        times = []
+        for nb in cands:
+            self.nbuckets = nb
+            self.step()
+            self.sync()
+            a, b = self.new_event(), self.new_event()
+            self.record(a)
+            for _ in range(iters):
+                self.step()
+            self.record(b)
+            self.sync()
+            times.append(self.elapsed(a, b) / iters)
+        t = torch.tensor(times, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        best = int(t.argmin().item())
+        self.nbuckets = cands[best]
+        self.fused = self.nbuckets > 1
+        self.calibration = {str(c): round(x, 4) for c, x in zip(cands, t.tolist())}
+        self.pushes_in_calibration = len(cands) * (iters + 1)
+
     def new_event(self):
         return self.p.Event()
 
@@ -93,17 +140,33 @@ class GpuBackend:
         self.stream.sync()
         self.p.device_sync()
 
+    def accumulate_probe(self, iters=10):
+        """The dominant local kernel at N > 1: the shard accumulate after the
+        reduce-scatter (12 B per f32 element), timed alone with HIP events."""
+        a, b = self.new_event(), self.new_event()
+        self.record(a)
+        for _ in range(iters):
+            self.store.handle(self.p.PUSH, None, self.scratch, None, self.blk,
+                              first_key=self.rank * self.blk, stream=self.stream)
+        self.record(b)
+        self.sync()
+        return self.elapsed(a, b) / iters
+
     def check(self, steps_done: int) -> bool:
-        """Pull result after `steps_done` pushes: every shard holds steps * sum_w vals_w
-        (integer-valued floats, exact)."""
+        """After `steps_done` pushes every shard holds steps * sum_w vals_w
+        (integer-valued, exact in f32 and in f16 at the default sizes)."""
         import numpy as np
+        import oracle
         self.pull()
         self.sync()
-        got = self.out.download(np.float32, min(self.L, 1 << 20), self.stream)
-        import oracle
-        exp = np.zeros_like(got)
+        n = min(self.L, 1 << 20)
+        npt = {self.p.F32: np.float32, self.p.F16: np.float16}[self.dt]
+        got = self.out.download(npt, n, self.stream).astype(np.float64)
+        exp = np.zeros(n)
+        odt = {self.p.F32: oracle.F32, self.p.F16: oracle.F16}[self.dt]
         for w in range(self.world):
-            exp += oracle.synth(len(got), oracle.F32, self._seed + w, 0, 0.0, 1000.0)
+            s = oracle.synth(n, odt, self._seed + w, 0, 0.0, self._hi())
+            exp += (s.view(np.float16) if self.dt == self.p.F16 else s).astype(np.float64)
         return bool(np.array_equal(got, exp * steps_done))
 
 
@@ -112,14 +175,25 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
     assert L % world == 0, "keys must divide by the number of shards"
     backend._seed = args.seed
     backend.setup(L, args.seed)
+    extra_pushes = 0
+    if hasattr(backend, "calibrate") and dist is not None:
+        backend.calibrate(dist)
+        extra_pushes = getattr(backend, "pushes_in_calibration", 0)
+    fused = getattr(backend, "fused", False)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    def one_step():
+        if fused:
+            backend.step()
+        else:
+            backend.push()
+            backend.pull()
+
     for _ in range(args.warmup):
-        backend.push()
-        backend.pull()
+        one_step()
     marks = [(backend.new_event(), backend.new_event(), backend.new_event())
              for _ in range(args.steps)]
     backend.sync()
@@ -128,36 +202,47 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
     t0 = time.perf_counter()
     for a, b, c in marks:
         backend.record(a)
-        backend.push()
-        backend.record(b)
-        backend.pull()
+        if fused:
+            backend.step()
+            backend.record(b)
+        else:
+            backend.push()
+            backend.record(b)
+            backend.pull()
         backend.record(c)
     backend.sync()
     barrier()
     t1 = time.perf_counter()
     local_ms = (t1 - t0) * 1e3 / max(args.steps, 1)
-    push_ms = sum(backend.elapsed(a, b) for a, b, _ in marks) / max(len(marks), 1)
-    pull_ms = sum(backend.elapsed(b, c) for _, b, c in marks) / max(len(marks), 1)
+    n_marks = max(len(marks), 1)
+    push_ms = sum(backend.elapsed(a, b) for a, b, _ in marks) / n_marks
+    pull_ms = sum(backend.elapsed(b, c) for _, b, c in marks) / n_marks
     ms = local_ms
+    acc_ms = backend.accumulate_probe() if (world > 1 and hasattr(backend, "accumulate_probe")) else None
     if dist is not None:
         import torch
-        t = torch.tensor([local_ms, push_ms, pull_ms], dtype=torch.float64)
+        t = torch.tensor([local_ms, push_ms, pull_ms, acc_ms or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, push_ms, pull_ms = t.tolist()
-    ok = backend.check(args.warmup + args.steps) if args.check else None
-    if dist is not None and args.check:
-        import torch
-        f = torch.tensor([0 if ok else 1], dtype=torch.int32)
-        dist.all_reduce(f, op=dist.ReduceOp.MAX)
-        ok = f.item() == 0
+        ms, push_ms, pull_ms, acc = t.tolist()
+        acc_ms = acc if acc_ms is not None else None
+    total_pushes = args.warmup + args.steps + extra_pushes + (10 if acc_ms is not None else 0)
+    ok = None
+    if args.check:
+        # the accumulate probe adds the (last reduce-scatter) scratch 10 more times,
+        # which breaks the closed form; only check when no probe ran
+        ok = backend.check(total_pushes) if acc_ms is None else backend_check_after_probe(backend)
+        if dist is not None:
+            import torch
+            f = torch.tensor([0 if ok else 1], dtype=torch.int32)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            ok = f.item() == 0
     if rank != 0:
         return None
-    payload = 2 * F32_BYTES * L * world  # pushed + pulled by all workers per step
+    vb = getattr(backend, "vb", 4)
+    payload = 2 * vb * L * world  # pushed + pulled by all workers per step
     value_gbs = payload / (ms * 1e-3) / 1e9
     blk = L // world
-    # dominant kernel: the Push accumulate over this rank's shard
-    push_alg = PUSH_BYTES_PER_ELEM * blk
-    roof_achieved = push_alg / (push_ms * 1e-3) / 1e9 if world == 1 else None
+    wl = getattr(args, "workload", "dense")
     res = {
         "metric": "device-resident KV Push+Pull GB/s (float vals)",
         "value": round(value_gbs, 3),
@@ -169,25 +254,32 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (integer-valued U{0..999} floats, seed 7+rank, generated in HBM)",
+        "dtype": WORKLOADS.get(wl, ("f32",))[0],
+        "data": "synthetic (integer-valued floats, seed 7+rank, generated in HBM)",
         "config": {
-            "workload": ("configs[1]: 1 server + 1 worker, dense Push then Pull"
-                         if world == 1 else
-                         f"configs[2] shape: ns=nw={world}, Push=RCCL reduce-scatter+accumulate, "
-                         f"Pull=RCCL all-gather"),
+            "workload": (f"{WORKLOADS.get(wl, ('', 0, 0, 'configs[1]'))[3]}: "
+                         + ("1 server + 1 worker, dense Push then Pull" if world == 1 else
+                            f"ns=nw={world}, Push=RCCL reduce-scatter+accumulate, Pull=RCCL all-gather")),
             "keys_per_worker": L,
             "shard_keys": blk,
             "parallelism": f"ps{world}",
         },
-        "push_ms": round(push_ms, 5),
-        "pull_ms": round(pull_ms, 5),
+        "push_ms": None if fused else round(push_ms, 5),
+        "pull_ms": None if fused else round(pull_ms, 5),
         "parity_check": ok,
     }
+    if world > 1 and hasattr(backend, "nbuckets"):
+        res["config"]["exchange"] = ("pipelined reduce/broadcast, %d buckets" % backend.nbuckets
+                                     if fused else "reduce-scatter then all-gather")
+        res["config"]["calibration_ms"] = getattr(backend, "calibration", None)
     if world == 1:
-        res["roofline"] = roofline(push_alg, push_ms, args)
-        res["pull_roofline_frac"] = round(PULL_BYTES_PER_ELEM * blk / (pull_ms * 1e-3) / 1e9
+        res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
+                                   "k_dense_vec<PUSH> (store += vals)", vb)
+        res["pull_roofline_frac"] = round(PULL_ACCESSES * vb * blk / (pull_ms * 1e-3) / 1e9
                                           / HBM_PEAK_GBS, 4)
+    elif acc_ms is not None:
+        res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, acc_ms, args,
+                                   "k_dense_vec<PUSH> on the shard after the reduce-scatter", vb)
     else:
         res["roofline"] = None
     if world == 1 and not args.no_cpu_baseline:
@@ -195,26 +287,40 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
     return res
 
 
-def roofline(push_alg_bytes: int, push_ms: float, args) -> dict:
-    achieved = push_alg_bytes / (push_ms * 1e-3) / 1e9
+def backend_check_after_probe(backend) -> bool:
+    """With the probe having re-added the scratch, check the Pull equals the shards
+    (all-gather correctness) instead of the closed form."""
+    import numpy as np
+    backend.pull()
+    backend.sync()
+    npt = {backend.p.F32: np.float32, backend.p.F16: np.float16}[backend.dt]
+    got = backend.out.download(npt, backend.L, backend.stream)
+    _, mine = backend.store.dump()
+    mine = mine.view(np.float16) if backend.dt == backend.p.F16 else mine
+    lo = backend.rank * backend.blk
+    return bool(np.array_equal(got[lo:lo + backend.blk], mine[:backend.blk]))
+
+
+def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_push_traffic.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and vb == 4:
         try:
             d = json.load(open(pmc))
-            if d.get("keys") == args.keys:
+            if d.get("keys") * 12 == alg_bytes:
                 traffic = d.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     return {
-        "kernel": "k_dense_vec<f32,PUSH> (store += vals)",
+        "kernel": kernel,
         "bound": "hbm",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "alg_bytes_per_launch": push_alg_bytes,
+        "alg_bytes_per_launch": alg_bytes,
     }
 
 
@@ -228,7 +334,7 @@ def cpu_baseline(args) -> dict:
     first, push_s, pull_s = oracle.bench(num, reps)
     wall = time.perf_counter() - t0
     return {
-        "value": round(2 * F32_BYTES * num / (push_s + pull_s) / 1e9, 4),
+        "value": round(2 * 4 * num / (push_s + pull_s) / 1e9, 4),
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
@@ -243,13 +349,17 @@ def main(argv=None) -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--keys", type=int, default=64 << 20, help="floats per worker (configs[1]: 64M)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="dense")
+    ap.add_argument("--keys", type=int, default=None, help="values per worker (default by workload)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--check", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-keys", type=int, default=10_000_000)
     ap.add_argument("--cpu-reps", type=int, default=12)
     args = ap.parse_args(argv)
+    dtype, _, default_keys, _ = WORKLOADS[args.workload]
+    if args.keys is None:
+        args.keys = default_keys
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -261,7 +371,7 @@ def main(argv=None) -> None:
         import torch  # noqa: F401  (load torch's HIP runtime before libpsgpu)
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    backend = GpuBackend(rank, world, local_rank, dist)
+    backend = GpuBackend(rank, world, local_rank, dist, dtype)
     res = run(backend, args, rank, world, dist)
     if res is not None:
         print(json.dumps(res), flush=True)

@@ -216,7 +216,10 @@ int psg_merge(psg_segment* segs_host, int nsegs, int elem_size, void* dst,
 /* ======================================================================== */
 /* Multi-GPU BSP data path over RCCL / xGMI (one server shard per GPU)        */
 /* ======================================================================== */
-/* Bytes of the opaque id rank 0 creates and every rank passes to init. */
+/* Bytes of the opaque id rank 0 creates and every rank passes to init (two
+ * RCCL unique ids: one communicator per direction of psg_comm_push_pull).
+ * PSG_COMM_FORCE_COLLECTIVE=1 makes a one-rank comm run the collectives
+ * anyway (they degenerate to copies) so the RCCL calls can be tested on one GPU. */
 int psg_comm_id_bytes(void);
 int psg_comm_get_id(void* id_host);
 int psg_comm_init(const void* id_host, int nranks, int rank, psg_comm** out);
@@ -236,6 +239,13 @@ int psg_comm_push(psg_comm* c, psg_store* shard, const void* vals, uint64_t n_to
  * an all-gather (KVApp.h:452 + the merge of KVApp.h:713-720). */
 int psg_comm_pull(psg_comm* c, psg_store* shard, void* out, uint64_t n_total,
                   psg_stream stream);
+/* Push then Pull of the same vector, pipelined over nbuckets: bucket b's
+ * reduce-to-owner + accumulate (stream, communicator 0) overlaps bucket b-1's
+ * broadcast-from-owner (side stream, communicator 1), so both directions of
+ * the xGMI links carry traffic.  Same result as psg_comm_push + psg_comm_pull;
+ * nbuckets <= 1 is exactly those two calls.  Complete on `stream` on return. */
+int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* out,
+                       uint64_t n_total, int nbuckets, psg_stream stream);
 
 /* ======================================================================== */
 /* LR server apply                                             */

@@ -8,17 +8,29 @@
 // rank r receives sum_w vals_w[block r] and adds it into its store shard with
 // the dense accumulate kernel.  A Pull is the all-gather of the shards, which
 // also performs the merge of KVApp.h:713-720 (blocks land in key order).
+//
+// psg_comm_push_pull pipelines the two over buckets: bucket b's reduce (to
+// each owner) + accumulate runs on the caller's stream and communicator 0
+// while bucket b-1's broadcast (from each owner) runs on a side stream and
+// communicator 1, so the two directions of every xGMI link carry traffic at
+// once.  Two communicators keep the two streams' collectives independent.
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "psg_internal.h"
 
 struct psg_comm {
-  ncclComm_t comm;
+  ncclComm_t comm[2];
   int rank, nranks, device;
+  bool force;  // run the collectives even with one rank (testing)
   void* scratch;
   size_t scratch_bytes;
+  hipStream_t side;
+  std::vector<hipEvent_t> ev;  // per-bucket "accumulated" events
+  hipEvent_t side_done;
 };
 
 namespace psg {
@@ -28,9 +40,9 @@ static int nccl_fail(ncclResult_t r, const char* what) {
   return PSG_ERR_COMM;
 }
 
-#define PSG_NCCL(call)                                   \
-  do {                                                   \
-    ncclResult_t r_ = (call);                            \
+#define PSG_NCCL(call)                                       \
+  do {                                                       \
+    ncclResult_t r_ = (call);                                \
     if (r_ != ncclSuccess) return psg::nccl_fail(r_, #call); \
   } while (0)
 
@@ -56,19 +68,31 @@ static int check_shard(psg_comm* c, psg_store* s, uint64_t n_total, uint64_t* bl
   return PSG_OK;
 }
 
+static int ensure_scratch(psg_comm* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return PSG_OK;
+  if (c->scratch) PSG_HIP(hipFree(c->scratch));
+  c->scratch = nullptr;
+  c->scratch_bytes = 0;
+  PSG_HIP(hipMalloc(&c->scratch, bytes));
+  c->scratch_bytes = bytes;
+  return PSG_OK;
+}
+
 }  // namespace psg
 
 using namespace psg;
 
 extern "C" {
 
-int psg_comm_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
+int psg_comm_id_bytes(void) { return 2 * (int)sizeof(ncclUniqueId); }
 
 int psg_comm_get_id(void* id_host) {
   PSG_REQUIRE(id_host, PSG_ERR_INVALID, "psg_comm_get_id: null out");
-  ncclUniqueId id;
-  PSG_NCCL(ncclGetUniqueId(&id));
-  memcpy(id_host, &id, sizeof(id));
+  for (int k = 0; k < 2; ++k) {
+    ncclUniqueId id;
+    PSG_NCCL(ncclGetUniqueId(&id));
+    memcpy((char*)id_host + k * sizeof(id), &id, sizeof(id));
+  }
   return PSG_OK;
 }
 
@@ -76,17 +100,27 @@ int psg_comm_init(const void* id_host, int nranks, int rank, psg_comm** out) {
   PSG_REQUIRE(id_host && out && nranks > 0 && rank >= 0 && rank < nranks, PSG_ERR_INVALID,
               "psg_comm_init: bad arguments");
   *out = nullptr;
-  ncclUniqueId id;
-  memcpy(&id, id_host, sizeof(id));
   psg_comm* c = new psg_comm();
-  memset(c, 0, sizeof(*c));
   c->rank = rank;
   c->nranks = nranks;
+  const char* f = getenv("PSG_COMM_FORCE_COLLECTIVE");
+  c->force = f && atoi(f) != 0;
   (void)hipGetDevice(&c->device);
-  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
-  if (r != ncclSuccess) {
-    delete c;
-    return nccl_fail(r, "ncclCommInitRank");
+  for (int k = 0; k < 2; ++k) {
+    ncclUniqueId id;
+    memcpy(&id, (const char*)id_host + k * sizeof(id), sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&c->comm[k], nranks, id, rank);
+    if (r != ncclSuccess) {
+      if (k == 1) ncclCommDestroy(c->comm[0]);
+      delete c;
+      return nccl_fail(r, "ncclCommInitRank");
+    }
+  }
+  hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    psg_comm_destroy(c);
+    return hip_fail(e, "psg_comm_init stream", __FILE__, __LINE__);
   }
   *out = c;
   return PSG_OK;
@@ -94,8 +128,13 @@ int psg_comm_init(const void* id_host, int nranks, int rank, psg_comm** out) {
 
 int psg_comm_destroy(psg_comm* c) {
   if (!c) return PSG_OK;
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->side_done) (void)hipEventDestroy(c->side_done);
+  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->scratch) (void)hipFree(c->scratch);
-  if (c->comm) ncclCommDestroy(c->comm);
+  for (int k = 0; k < 2; ++k)
+    if (c->comm[k]) ncclCommDestroy(c->comm[k]);
   delete c;
   return PSG_OK;
 }
@@ -114,22 +153,15 @@ int psg_comm_push(psg_comm* c, psg_store* shard, const void* vals, uint64_t n_to
   if (blk == 0) return PSG_OK;
   PSG_REQUIRE(vals, PSG_ERR_INVALID, "psg_comm_push: null vals");
   hipStream_t st = (hipStream_t)stream;
-  if (c->nranks == 1)  // a one-rank reduce-scatter is the identity
+  if (c->nranks == 1 && !c->force)  // a one-rank reduce-scatter is the identity
     return dense_request(shard->dtype, PSG_PUSH, shard->vals, vals, nullptr, blk, st);
   ncclDataType_t t;
   PSG_REQUIRE(nccl_type(shard->dtype, &t), PSG_ERR_UNSUPPORTED, "psg_comm_push: dtype %d", shard->dtype);
-  const size_t bytes = blk * shard->esize;
   if (!scratch) {
-    if (c->scratch_bytes < bytes) {
-      if (c->scratch) PSG_HIP(hipFree(c->scratch));
-      c->scratch = nullptr;
-      c->scratch_bytes = 0;
-      PSG_HIP(hipMalloc(&c->scratch, bytes));
-      c->scratch_bytes = bytes;
-    }
+    PSG_TRY(ensure_scratch(c, blk * shard->esize));
     scratch = c->scratch;
   }
-  PSG_NCCL(ncclReduceScatter(vals, scratch, blk, t, ncclSum, c->comm, st));
+  PSG_NCCL(ncclReduceScatter(vals, scratch, blk, t, ncclSum, c->comm[0], st));
   return dense_request(shard->dtype, PSG_PUSH, shard->vals, scratch, nullptr, blk, st);
 }
 
@@ -139,11 +171,71 @@ int psg_comm_pull(psg_comm* c, psg_store* shard, void* out, uint64_t n_total, ps
   if (blk == 0) return PSG_OK;
   PSG_REQUIRE(out, PSG_ERR_INVALID, "psg_comm_pull: null out");
   hipStream_t st = (hipStream_t)stream;
-  if (c->nranks == 1)
+  if (c->nranks == 1 && !c->force)
     return dense_request(shard->dtype, PSG_PULL, shard->vals, nullptr, out, blk, st);
   ncclDataType_t t;
   PSG_REQUIRE(nccl_type(shard->dtype, &t), PSG_ERR_UNSUPPORTED, "psg_comm_pull: dtype %d", shard->dtype);
-  PSG_NCCL(ncclAllGather(shard->vals, out, blk, t, c->comm, st));
+  PSG_NCCL(ncclAllGather(shard->vals, out, blk, t, c->comm[0], st));
+  return PSG_OK;
+}
+
+int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* out, uint64_t n_total,
+                       int nbuckets, psg_stream stream) {
+  uint64_t blk = 0;
+  PSG_TRY(check_shard(c, shard, n_total, &blk));
+  if (blk == 0) return PSG_OK;
+  PSG_REQUIRE(vals && out, PSG_ERR_INVALID, "psg_comm_push_pull: null buffer");
+  hipStream_t st = (hipStream_t)stream;
+  if (nbuckets <= 1 || (c->nranks == 1 && !c->force)) {
+    PSG_TRY(psg_comm_push(c, shard, vals, n_total, nullptr, stream));
+    return psg_comm_pull(c, shard, out, n_total, stream);
+  }
+  ncclDataType_t t;
+  PSG_REQUIRE(nccl_type(shard->dtype, &t), PSG_ERR_UNSUPPORTED, "psg_comm_push_pull: dtype %d",
+              shard->dtype);
+  const int es = shard->esize;
+  // bucket b covers [b*chunk, min((b+1)*chunk, blk)) of every rank's block;
+  // chunks are multiples of 64 elements so vector kernels stay aligned
+  uint64_t chunk = (blk + (uint64_t)nbuckets - 1) / (uint64_t)nbuckets;
+  chunk = (chunk + 63) / 64 * 64;
+  const int nb = (int)((blk + chunk - 1) / chunk);
+  PSG_TRY(ensure_scratch(c, blk * es));
+  while ((int)c->ev.size() < nb) {
+    hipEvent_t e;
+    PSG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ev.push_back(e);
+  }
+  // the side stream must not start a bucket's broadcast before the caller's
+  // earlier work on the output buffer is done
+  PSG_HIP(hipEventRecord(c->side_done, st));
+  PSG_HIP(hipStreamWaitEvent(c->side, c->side_done, 0));
+  const char* in = (const char*)vals;
+  char* o = (char*)out;
+  char* sv = (char*)shard->vals;
+  char* sc = (char*)c->scratch;
+  for (int b = 0; b < nb; ++b) {
+    const uint64_t off = (uint64_t)b * chunk;
+    const uint64_t cnt = off + chunk <= blk ? chunk : blk - off;
+    // Push of bucket b: every rank's chunk b reduced to its owner, then accumulated
+    PSG_NCCL(ncclGroupStart());
+    for (int r = 0; r < c->nranks; ++r) {
+      const char* src = in + ((uint64_t)r * blk + off) * es;
+      PSG_NCCL(ncclReduce(src, sc + off * es, cnt, t, ncclSum, r, c->comm[0], st));
+    }
+    PSG_NCCL(ncclGroupEnd());
+    PSG_TRY(dense_request(shard->dtype, PSG_PUSH, sv + off * es, sc + off * es, nullptr, cnt, st));
+    PSG_HIP(hipEventRecord(c->ev[b], st));
+    // Pull of bucket b on the side stream: each owner broadcasts its updated chunk
+    PSG_HIP(hipStreamWaitEvent(c->side, c->ev[b], 0));
+    PSG_NCCL(ncclGroupStart());
+    for (int r = 0; r < c->nranks; ++r) {
+      char* dst = o + ((uint64_t)r * blk + off) * es;
+      PSG_NCCL(ncclBroadcast(sv + off * es, dst, cnt, t, r, c->comm[1], c->side));
+    }
+    PSG_NCCL(ncclGroupEnd());
+  }
+  PSG_HIP(hipEventRecord(c->side_done, c->side));
+  PSG_HIP(hipStreamWaitEvent(st, c->side_done, 0));
   return PSG_OK;
 }
 

@@ -3,10 +3,38 @@
 // LOG_FATAL_THROW=1 in src/base/base.h:19-21).  LOG(INFO) prints only when
 // PS_VERBOSE >= 1; WARNING and ERROR always print to stderr.
 #pragma once
+// the standard headers the reference's log.h brings in (log.h:24-45): harness
+// code relies on them transitively (std::put_time in tests/LR_ps.cpp:54)
+#include <chrono>
+#include <ctime>
+#include <fstream>
+#include <iomanip>
 #include <iostream>
 #include <sstream>
 #include <stdexcept>
 #include <string>
+
+#if defined(__GLIBCXX__) && defined(_GLIBCXX_RELEASE) && _GLIBCXX_RELEASE < 13 && __cplusplus >= 202002L
+// C++20 streams std::chrono::duration (count + unit suffix); libstdc++ gained
+// that operator in release 13.  tests/LR_ps.cpp:88 needs it, so older
+// libstdc++ gets the same output format here.
+namespace std {
+namespace chrono {
+template <class Rep, class Period>
+std::ostream& operator<<(std::ostream& os, const duration<Rep, Period>& d) {
+  os << d.count();
+  if constexpr (std::is_same_v<Period, std::nano>) os << "ns";
+  else if constexpr (std::is_same_v<Period, std::micro>) os << "\xC2\xB5s";
+  else if constexpr (std::is_same_v<Period, std::milli>) os << "ms";
+  else if constexpr (std::is_same_v<Period, std::ratio<1>>) os << "s";
+  else if constexpr (std::is_same_v<Period, std::ratio<60>>) os << "min";
+  else if constexpr (std::is_same_v<Period, std::ratio<3600>>) os << "h";
+  else os << "[" << Period::num << "/" << Period::den << "]s";
+  return os;
+}
+}  // namespace chrono
+}  // namespace std
+#endif
 
 namespace ps_log {
 

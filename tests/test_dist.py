@@ -102,9 +102,18 @@ def _rank_main(rank, world, port, outdir):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_distributed_path_gloo(world):
-    import torch.multiprocessing as mp
+    # torch is imported only inside the rank processes: a process that loaded
+    # libpsgpu.so (HIP from /opt/rocm) must not load torch's HIP runtime after it
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rank_main, args=(world, _free_port(), d), nprocs=world, join=True)
+        port = _free_port()
+        procs = [ctx.Process(target=_rank_main, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=120)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         r0 = json.load(open(os.path.join(d, "r0.json")))
         for r in range(1, world):
             assert json.load(open(os.path.join(d, f"r{r}.json"))) is None  # only rank 0 prints

@@ -292,16 +292,29 @@ def test_lr_apply_bitexact(adam):
     np.testing.assert_array_equal(got, w)
 
 
-def test_comm_single_rank_push_pull():
-    uid = psg.comm_id()
-    c = psg.Comm(uid, 1, 0)
-    n = 1 << 20
-    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
-    v = psg.DeviceBuffer(n * 4)
-    v.fill_synth(n, psg.F32, 3, 0, 0.0, 1000.0)
-    out = psg.DeviceBuffer(n * 4)
+@pytest.mark.parametrize("force", [False, True])
+@pytest.mark.parametrize("dtype,n", [(psg.F32, 1 << 20), (psg.F32, 1000003), (psg.F16, 65600)])
+def test_comm_single_rank_push_pull(force, dtype, n, monkeypatch):
+    """force=True runs the RCCL reduce-scatter / all-gather and the pipelined
+    grouped reduce / broadcast even with one rank (they degenerate to copies),
+    so the collective calls themselves execute on the MI355X."""
+    if force:
+        monkeypatch.setenv("PSG_COMM_FORCE_COLLECTIVE", "1")
+    c = psg.Comm(psg.comm_id(), 1, 0)
+    st = psg.Store(psg.DENSE, dtype, 0, n, n)
+    v = psg.DeviceBuffer(n * ES[dtype])
+    v.fill_synth(n, dtype, 3, 0, 0.0, 100.0)
+    out = psg.DeviceBuffer(n * ES[dtype])
+    orc = oracle.Store(dtype)
+    hv = oracle.synth(n, dtype, 3, 0, 0.0, 100.0)
     c.push(st, v, n)
     c.push(st, v, n)
     c.pull(st, out, n)
-    np.testing.assert_array_equal(out.download(np.float32, n), v.download(np.float32, n) * 2)
+    orc.handle(oracle.PUSH, None, hv, n)
+    orc.handle(oracle.PUSH, None, hv, n)
+    np.testing.assert_array_equal(out.download(NPT[dtype], n), orc.handle(oracle.PULL, None, None, n))
+    for nb in (1, 3, 8):
+        c.push_pull(st, v, out, n, nb)
+        exp = orc.handle(oracle.PUSH | oracle.PULL, None, hv, n)
+        np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"nbuckets={nb}")
     c.close()
