@@ -43,18 +43,25 @@ WORKLOADS = {
     # name: (dtype name, value bytes, default values per worker, description)
     "dense": ("f32", 4, 64 << 20, "configs[1]"),
     "dense-f16": ("f16", 2, 1 << 30, "configs[4]"),
+    "keyed": ("f32", 4, 10_000_000, "configs[3]"),
 }
+# algorithmic HBM bytes per key of one keyed Push on the SORTED store:
+# request key 8 + store key 8 (resolve) + slot write 4 + slot read 4 + value 4
+# + store value read/write 8
+KEYED_PUSH_BYTES = 36
 
 
 class GpuBackend:
     """The product path: psg C-ABI (HIP kernels + RCCL)."""
 
-    def __init__(self, rank: int, world: int, local_rank: int, dist=None, dtype="f32"):
+    def __init__(self, rank: int, world: int, local_rank: int, dist=None, dtype="f32",
+                 keyed=False):
         import psg
         self.p = psg
         self.rank, self.world, self.dist = rank, world, dist
         self.dt = {"f32": psg.F32, "f16": psg.F16}[dtype]
         self.vb = {"f32": 4, "f16": 2}[dtype]
+        self.keyed = keyed
         psg.set_device(local_rank)
         self.stream = psg.Stream()
         self.comm = None
@@ -66,9 +73,21 @@ class GpuBackend:
         blk = L // self.world
         self.L, self.blk, self._seed = L, blk, seed
         lo = self.rank * blk
-        self.store = p.Store(p.DENSE, self.dt, lo, lo + blk, blk)
+        if self.keyed:
+            # configs[3]: L unique sorted uint64 keys drawn uniformly (seed 9), the same
+            # key set on every worker (LR-like); each server keeps a SORTED store
+            import numpy as np
+            rng = np.random.default_rng(9)
+            k = np.unique(rng.integers(0, (1 << 64) - 1, int(L * 1.01) + 1024, dtype=np.uint64))
+            k = np.sort(rng.choice(k, L, replace=False)) if len(k) > L else k
+            self.keys = p.DeviceBuffer.from_numpy(k.astype(np.uint64))
+            self.begins, self.ends = p.server_ranges(self.world)
+            self.store = p.Store(p.SORTED, self.dt, int(self.begins[self.rank]),
+                                 int(self.ends[self.rank]), 0)
+        else:
+            self.store = p.Store(p.DENSE, self.dt, lo, lo + blk, blk)
         self.vals = p.DeviceBuffer(L * self.vb)
-        # integer-valued 0..99 (f16 holds them and their sums exactly) / 0..999 (f32)
+        # integer-valued 0..7 (f16 holds them and their sums exactly) / 0..999 (f32)
         self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self._hi(), self.stream)
         self.out = p.DeviceBuffer(L * self.vb)
         if self.world > 1:
@@ -78,19 +97,36 @@ class GpuBackend:
             self.scratch = p.DeviceBuffer(blk * self.vb)
         self.sync()
 
+    def _key_pos(self):
+        # the worker's DefaultSlicer on its HBM keys (psg_slice), every request
+        kp, _ = self.p.slice_keys(self.keys, self.L, self.begins, self.ends, stream=self.stream)
+        return kp
+
     def _hi(self):
         return 1000.0 if self.dt == self.p.F32 else 8.0
 
     # -- one phase at a time (N = 1, or the sequential RS / AG at N > 1)
     def push(self):
-        if self.comm is None:
+        if self.keyed:
+            kp = self._key_pos()
+            if self.comm is None:
+                self.store.handle(self.p.PUSH, self.keys, self.vals, None, self.L, stream=self.stream)
+            else:
+                self.comm.push_keyed(self.store, self.keys, self.vals, self.L, kp, self.stream)
+        elif self.comm is None:
             self.store.handle(self.p.PUSH, None, self.vals, None, self.L, first_key=0,
                               stream=self.stream)
         else:
             self.comm.push(self.store, self.vals, self.L, self.scratch, self.stream)
 
     def pull(self):
-        if self.comm is None:
+        if self.keyed:
+            kp = self._key_pos()
+            if self.comm is None:
+                self.store.handle(self.p.PULL, self.keys, None, self.out, self.L, stream=self.stream)
+            else:
+                self.comm.pull_keyed(self.store, self.keys, self.out, self.L, kp, self.stream)
+        elif self.comm is None:
             self.store.handle(self.p.PULL, None, None, self.out, self.L, first_key=0,
                               stream=self.stream)
         else:
@@ -103,7 +139,7 @@ class GpuBackend:
     def calibrate(self, dist, iters=3):
         """Pick sequential RS+AG (nbuckets 1) or a pipelined bucket count by timing
         each a few times; the max over ranks decides, so every rank picks the same."""
-        if self.comm is None:
+        if self.comm is None or self.keyed:
             return
         import torch
         cands = [1, 4, 8, 16]
@@ -143,6 +179,8 @@ class GpuBackend:
     def accumulate_probe(self, iters=10):
         """The dominant local kernel at N > 1: the shard accumulate after the
         reduce-scatter (12 B per f32 element), timed alone with HIP events."""
+        if self.keyed:
+            return None
         a, b = self.new_event(), self.new_event()
         self.record(a)
         for _ in range(iters):
@@ -258,8 +296,9 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         "data": "synthetic (integer-valued floats, seed 7+rank, generated in HBM)",
         "config": {
             "workload": (f"{WORKLOADS.get(wl, ('', 0, 0, 'configs[1]'))[3]}: "
-                         + ("1 server + 1 worker, dense Push then Pull" if world == 1 else
-                            f"ns=nw={world}, Push=RCCL reduce-scatter+accumulate, Pull=RCCL all-gather")),
+                         + (("keyed (10 M sorted uint64 keys, SORTED store), " if wl == "keyed" else "dense, ")
+                            + ("1 server + 1 worker, Push then Pull" if world == 1 else
+                               f"ns=nw={world}, BSP Push/Pull over RCCL"))),
             "keys_per_worker": L,
             "shard_keys": blk,
             "parallelism": f"ps{world}",
@@ -272,7 +311,11 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         res["config"]["exchange"] = ("pipelined reduce/broadcast, %d buckets" % backend.nbuckets
                                      if fused else "reduce-scatter then all-gather")
         res["config"]["calibration_ms"] = getattr(backend, "calibration", None)
-    if world == 1:
+    if world == 1 and getattr(backend, "keyed", False):
+        res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
+                                   "SORTED-store Push: psg_slice + k_tile_windows + k_resolve + "
+                                   "k_slots (one host sync)", vb)
+    elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
                                    "k_dense_vec<PUSH> (store += vals)", vb)
         res["pull_roofline_frac"] = round(PULL_ACCESSES * vb * blk / (pull_ms * 1e-3) / 1e9
@@ -371,7 +414,7 @@ def main(argv=None) -> None:
         import torch  # noqa: F401  (load torch's HIP runtime before libpsgpu)
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    backend = GpuBackend(rank, world, local_rank, dist, dtype)
+    backend = GpuBackend(rank, world, local_rank, dist, dtype, keyed=args.workload == "keyed")
     res = run(backend, args, rank, world, dist)
     if res is not None:
         print(json.dumps(res), flush=True)

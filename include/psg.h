@@ -247,6 +247,19 @@ int psg_comm_pull(psg_comm* c, psg_store* shard, void* out, uint64_t n_total,
 int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* out,
                        uint64_t n_total, int nbuckets, psg_stream stream);
 
+/* Keyed BSP Push / Pull (configs[3], LR_ps): every rank passes the SAME sorted
+ * key array keys[n] (device) and its values; key_pos_host[nranks+1] are the
+ * psg_slice bounds of the server ranges (key_pos[0] = 0, key_pos[nranks] = n).
+ * Push: segment r of every rank's vals is reduced to rank r and applied to its
+ * store (SORTED or DENSE) with psg_store_handle — the nranks x nranks Push
+ * messages of KVWorker::Send (KVApp.h:596-618) as one grouped RCCL reduce.
+ * Pull: each owner reads its segment into out[key_pos[r]..] and broadcasts
+ * it, which also does the merge of KVApp.h:713-720. */
+int psg_comm_push_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, const void* vals,
+                        uint64_t n, const uint64_t* key_pos_host, psg_stream stream);
+int psg_comm_pull_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, void* out,
+                        uint64_t n, const uint64_t* key_pos_host, psg_stream stream);
+
 /* ======================================================================== */
 /* LR server apply                                             */
 /* ======================================================================== */

@@ -239,4 +239,77 @@ int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* ou
   return PSG_OK;
 }
 
+// ---- keyed BSP (configs[3], LR_ps): every rank pushes values for the SAME
+// sorted key array, cut by psg_slice into per-server segments key_pos[r] ..
+// key_pos[r+1].  Push: segment r of every rank is reduced to rank r, which
+// applies it to its store with the keyed handle; Pull: every owner reads its
+// segment and broadcasts it into place.
+static int keyed_args(psg_comm* c, psg_store* s, const uint64_t* keys, uint64_t n,
+                      const uint64_t* kp, uint64_t* maxseg) {
+  PSG_REQUIRE(c && s && kp, PSG_ERR_INVALID, "psg_comm keyed: null argument");
+  PSG_REQUIRE(n == 0 || keys, PSG_ERR_INVALID, "psg_comm keyed: null keys");
+  PSG_REQUIRE(kp[0] == 0 && kp[c->nranks] == n, PSG_ERR_INVALID,
+              "psg_comm keyed: key_pos must cover [0, n) (%llu..%llu vs %llu)",
+              (unsigned long long)kp[0], (unsigned long long)kp[c->nranks], (unsigned long long)n);
+  *maxseg = 0;
+  for (int r = 0; r < c->nranks; ++r) {
+    PSG_REQUIRE(kp[r] <= kp[r + 1], PSG_ERR_INVALID, "psg_comm keyed: key_pos not ascending");
+    if (kp[r + 1] - kp[r] > *maxseg) *maxseg = kp[r + 1] - kp[r];
+  }
+  return PSG_OK;
+}
+
+int psg_comm_push_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, const void* vals,
+                        uint64_t n, const uint64_t* key_pos_host, psg_stream stream) {
+  uint64_t maxseg = 0;
+  PSG_TRY(keyed_args(c, shard, keys, n, key_pos_host, &maxseg));
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(vals, PSG_ERR_INVALID, "psg_comm_push_keyed: null vals");
+  const int me = c->rank, es = shard->esize;
+  const uint64_t* kp = key_pos_host;
+  const uint64_t mine = kp[me + 1] - kp[me];
+  if (c->nranks == 1 && !c->force)
+    return psg_store_handle(shard, PSG_PUSH, keys, 0, vals, nullptr, n, stream);
+  hipStream_t st = (hipStream_t)stream;
+  ncclDataType_t t;
+  PSG_REQUIRE(nccl_type(shard->dtype, &t), PSG_ERR_UNSUPPORTED, "psg_comm_push_keyed: dtype %d",
+              shard->dtype);
+  PSG_TRY(ensure_scratch(c, (maxseg ? maxseg : 1) * es));
+  PSG_NCCL(ncclGroupStart());
+  for (int r = 0; r < c->nranks; ++r) {
+    const uint64_t cnt = kp[r + 1] - kp[r];
+    if (cnt) PSG_NCCL(ncclReduce((const char*)vals + kp[r] * es, c->scratch, cnt, t, ncclSum, r, c->comm[0], st));
+  }
+  PSG_NCCL(ncclGroupEnd());
+  if (!mine) return PSG_OK;
+  return psg_store_handle(shard, PSG_PUSH, keys + kp[me], 0, c->scratch, nullptr, mine, stream);
+}
+
+int psg_comm_pull_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, void* out, uint64_t n,
+                        const uint64_t* key_pos_host, psg_stream stream) {
+  uint64_t maxseg = 0;
+  PSG_TRY(keyed_args(c, shard, keys, n, key_pos_host, &maxseg));
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(out, PSG_ERR_INVALID, "psg_comm_pull_keyed: null out");
+  const int me = c->rank, es = shard->esize;
+  const uint64_t* kp = key_pos_host;
+  const uint64_t mine = kp[me + 1] - kp[me];
+  if (mine)
+    PSG_TRY(psg_store_handle(shard, PSG_PULL, keys + kp[me], 0, nullptr, (char*)out + kp[me] * es, mine,
+                             stream));
+  if (c->nranks == 1 && !c->force) return PSG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  ncclDataType_t t;
+  PSG_REQUIRE(nccl_type(shard->dtype, &t), PSG_ERR_UNSUPPORTED, "psg_comm_pull_keyed: dtype %d",
+              shard->dtype);
+  PSG_NCCL(ncclGroupStart());
+  for (int r = 0; r < c->nranks; ++r) {
+    const uint64_t cnt = kp[r + 1] - kp[r];
+    char* p = (char*)out + kp[r] * es;
+    if (cnt) PSG_NCCL(ncclBroadcast(p, p, cnt, t, r, c->comm[0], st));
+  }
+  PSG_NCCL(ncclGroupEnd());
+  return PSG_OK;
+}
+
 }  // extern "C"

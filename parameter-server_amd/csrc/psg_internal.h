@@ -136,6 +136,8 @@ struct psg_store {
   uint64_t* keys;     // device, SORTED only
   // scratch for SORTED requests (grown on demand)
   uint32_t* slots;
+  uint32_t* slots2;  // slots after an insert (second resolve)
+  uint64_t* wlo;     // per-tile store-key windows of the resolve
   uint64_t slots_cap;
   int* flags;        // device int[4]: missing count, contiguous flag, ...
   int* flags_host;   // pinned mirror

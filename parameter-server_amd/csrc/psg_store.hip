@@ -40,35 +40,79 @@ __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__
   return lo;
 }
 
-// Resolve sorted request keys q[0..n) against K[0..S).  slots[i] = index of
-// q[i] in K, or kNoSlot.  flags: [F_MISSING] += absent keys, [F_NONCONTIG] |=
-// slots not equal to base + i, [F_RANGE] |= key outside [kb, ke),
-// [F_UNSORTED] |= q not strictly ascending.
+constexpr int kWin = 4096;  // LDS-staged window of store keys (32 KiB)
+
+// Pass 1: the store-key window of every 1024-key request tile, one lane per
+// tile (all searches in flight at once instead of two per block in turn):
+// wlo[t] = lower_bound(K, q[t * kTile]); wlo[ntiles] = lower_bound(K, q[n-1]) + 1.
+__global__ __launch_bounds__(256) void k_tile_windows(const uint64_t* __restrict__ q, uint64_t n,
+                                                      const uint64_t* __restrict__ K, uint64_t S,
+                                                      uint64_t* __restrict__ wlo) {
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t <= ntiles;
+       t += (uint64_t)gridDim.x * kBlock) {
+    if (t < ntiles) {
+      wlo[t] = lower_bound_dev(K, 0, S, q[t * kTile]);
+    } else {
+      const uint64_t h = lower_bound_dev(K, 0, S, q[n - 1]);
+      wlo[t] = h < S ? h + 1 : S;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lower_bound_lds(const uint64_t* a, uint32_t w, uint64_t key) {
+  uint32_t lo = 0, hi = w;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Pass 2: resolve sorted request keys q[0..n) against K[0..S).  Each block
+// stages its tile's window of K into LDS with coalesced loads and binary-
+// searches there (a global search only when a sparse request leaves a window
+// wider than kWin).  slots[i] = index of q[i] in K, or kNoSlot.  flags:
+// [F_MISSING] += absent keys, [F_NONCONTIG] |= slots not equal to base + i,
+// [F_RANGE] |= key outside [kb, ke), [F_UNSORTED] |= q not strictly ascending.
+// A slot is only written when K[slot] == key, so unsorted input never
+// produces a wrong slot (it is flagged and the request rejected).
 __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q, uint64_t n,
                                                  const uint64_t* __restrict__ K, uint64_t S,
-                                                 uint64_t kb, uint64_t ke,
-                                                 uint32_t* __restrict__ slots,
+                                                 const uint64_t* __restrict__ wlo, uint64_t kb,
+                                                 uint64_t ke, uint32_t* __restrict__ slots,
                                                  int* __restrict__ flags) {
-  __shared__ uint64_t win[3];
+  __shared__ uint64_t sK[kWin];
   int missing = 0, noncontig = 0, range = 0, unsorted = 0;
   const uint64_t ntiles = (n + kTile - 1) / kTile;
+  const uint64_t base = wlo[0];
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * kTile;
     const uint64_t t1 = (t0 + kTile < n) ? t0 + kTile : n;
-    if (threadIdx.x == 0) win[0] = lower_bound_dev(K, 0, S, q[t0]);
-    if (threadIdx.x == 64) {
-      uint64_t hi = lower_bound_dev(K, 0, S, q[t1 - 1]);
-      win[1] = hi < S ? hi + 1 : S;
-    }
-    if (threadIdx.x == 128) win[2] = lower_bound_dev(K, 0, S, q[0]);
+    const uint64_t lo = wlo[tile];
+    uint64_t hi = tile + 1 < ntiles ? wlo[tile + 1] + 1 : wlo[ntiles];
+    if (hi > S) hi = S;
+    if (hi < lo) hi = lo;  // unsorted input
+    const uint64_t W = hi - lo;
+    const bool staged = W <= (uint64_t)kWin;
+    if (staged)
+      for (uint64_t j = threadIdx.x; j < W; j += kBlock) sK[j] = K[lo + j];
     __syncthreads();
-    const uint64_t lo = win[0], hi = win[1], base = win[2];
     for (uint64_t i = t0 + threadIdx.x; i < t1; i += kBlock) {
       const uint64_t key = q[i];
       if (key < kb || key >= ke) range = 1;
       if (i > 0 && q[i - 1] >= key) unsorted = 1;
-      const uint64_t p = lower_bound_dev(K, lo, hi, key);
-      const bool found = p < S && K[p] == key;
+      uint64_t p;
+      bool found;
+      if (staged) {
+        const uint32_t r = lower_bound_lds(sK, (uint32_t)W, key);
+        p = lo + r;
+        found = r < W && sK[r] == key;
+      } else {
+        p = lower_bound_dev(K, lo, hi, key);
+        found = p < S && K[p] == key;
+      }
       slots[i] = found ? (uint32_t)p : kNoSlot;
       if (!found) missing++;
       if (!found || p != base + i) noncontig = 1;
@@ -249,10 +293,80 @@ static unsigned grid_n(uint64_t n, uint64_t per_block) {
 static int ensure_slots(psg_store* s, uint64_t n) {
   if (s->slots_cap >= n) return PSG_OK;
   if (s->slots) PSG_HIP(hipFree(s->slots));
-  s->slots = nullptr;
+  if (s->slots2) PSG_HIP(hipFree(s->slots2));
+  if (s->wlo) PSG_HIP(hipFree(s->wlo));
+  s->slots = s->slots2 = nullptr;
+  s->wlo = nullptr;
+  s->slots_cap = 0;
   uint64_t cap = std::max<uint64_t>(n, 1 << 16);
   PSG_HIP(hipMalloc(&s->slots, cap * sizeof(uint32_t)));
+  PSG_HIP(hipMalloc(&s->slots2, cap * sizeof(uint32_t)));
+  PSG_HIP(hipMalloc(&s->wlo, (cap / kTile + 2) * sizeof(uint64_t)));
   s->slots_cap = cap;
+  return PSG_OK;
+}
+
+// Launch the two resolve passes for q into `slots` (no host sync).
+static int launch_resolve(psg_store* s, const uint64_t* q, uint64_t n, uint32_t* slots,
+                          hipStream_t st) {
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+  k_tile_windows<<<grid_n(ntiles + 1, kBlock), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
+  k_resolve<<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
+                                                  s->key_end, slots, s->flags);
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+static int check_request_flags(psg_store* s) {
+  const int* f = s->flags_host;
+  PSG_REQUIRE(!f[F_UNSORTED], PSG_ERR_INVALID,
+              "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
+  PSG_REQUIRE(!f[F_RANGE], PSG_ERR_RANGE, "request key outside the store range [%llu, %llu)",
+              (unsigned long long)s->key_begin, (unsigned long long)s->key_end);
+  return PSG_OK;
+}
+
+// Apply the request to the keys that were absent in the first pass
+// (old[i] == kNoSlot), now inserted at new[i].
+template <int DT, int OP>
+__global__ __launch_bounds__(256) void k_slots_fixup(typename Elem<DT>::T* __restrict__ store,
+                                                     const uint32_t* __restrict__ old_slots,
+                                                     const uint32_t* __restrict__ new_slots,
+                                                     const typename Elem<DT>::T* __restrict__ vals,
+                                                     typename Elem<DT>::T* __restrict__ out,
+                                                     uint64_t n) {
+  using E = Elem<DT>;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlock) {
+    if (old_slots[i] != kNoSlot) continue;
+    const uint32_t p = new_slots[i];
+    typename E::T v = store[p];
+    if constexpr ((OP & PSG_PUSH) != 0) {
+      v = E::add1(v, vals[i]);
+      store[p] = v;
+    }
+    if constexpr ((OP & PSG_PULL) != 0) out[i] = v;
+  }
+}
+
+template <int DT>
+static int run_fixup(psg_store* s, int op, const void* vals, void* out, uint64_t n, hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  const unsigned g = grid_n(n, kBlock);
+  T* sv = (T*)s->vals;
+  switch (op) {
+    case PSG_PUSH:
+      k_slots_fixup<DT, PSG_PUSH><<<g, kBlock, 0, st>>>(sv, s->slots, s->slots2, (const T*)vals, (T*)out, n);
+      break;
+    case PSG_PULL:
+      k_slots_fixup<DT, PSG_PULL><<<g, kBlock, 0, st>>>(sv, s->slots, s->slots2, (const T*)vals, (T*)out, n);
+      break;
+    default:
+      k_slots_fixup<DT, PSG_PUSH | PSG_PULL><<<g, kBlock, 0, st>>>(sv, s->slots, s->slots2,
+                                                                  (const T*)vals, (T*)out, n);
+  }
+  PSG_HIP(hipGetLastError());
   return PSG_OK;
 }
 
@@ -312,39 +426,45 @@ static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, uint64_t 
   return rc;
 }
 
-// Resolve q against the SORTED store, inserting absent keys when asked.
-// On return s->slots[0..n) holds the slots; *contig_base = slot of q[0] when
-// the slots are one contiguous run (else UINT64_MAX).
-static int sorted_resolve(psg_store* s, const uint64_t* q, uint64_t n, bool insert,
-                          uint64_t* contig_base, hipStream_t st) {
+// One request on the SORTED store with ONE host synchronisation in the steady
+// state: resolve (2 kernels) -> gather/scatter over the slots (absent keys
+// skipped; a pull of an absent key reads 0, which is what its insertion
+// gives) -> read the flags.  Only when keys were absent: insert them (merge),
+// resolve again into slots2, and apply the request to exactly those keys.
+static int sorted_request(psg_store* s, int op, const uint64_t* q, const void* vals, void* out,
+                          uint64_t n, hipStream_t st) {
   PSG_TRY(ensure_slots(s, n));
-  for (int pass = 0; pass < 2; ++pass) {
-    PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
-    const uint64_t ntiles = (n + kTile - 1) / kTile;
-    k_resolve<<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size, s->key_begin,
-                                                    s->key_end, s->slots, s->flags);
-    PSG_HIP(hipGetLastError());
-    PSG_TRY(read_flags(s, st));
-    const int* f = s->flags_host;
-    PSG_REQUIRE(!f[F_UNSORTED], PSG_ERR_INVALID,
-                "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
-    PSG_REQUIRE(!f[F_RANGE], PSG_ERR_RANGE, "request key outside the store range [%llu, %llu)",
-                (unsigned long long)s->key_begin, (unsigned long long)s->key_end);
-    if (f[F_MISSING] == 0 || !insert) {
-      if (contig_base) {
-        *contig_base = UINT64_MAX;
-        if (!f[F_NONCONTIG] && f[F_MISSING] == 0) {
-          uint32_t p0;
-          PSG_HIP(hipMemcpyAsync(&p0, s->slots, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-          PSG_HIP(hipStreamSynchronize(st));
-          *contig_base = p0;
-        }
-      }
-      return PSG_OK;
-    }
-    PSG_REQUIRE(pass == 0, PSG_ERR_HIP, "SORTED store: keys still absent after insert");
-    PSG_TRY(insert_missing(s, q, n, (uint64_t)f[F_MISSING], st));
+  PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+  PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
+  PSG_TRY(read_flags(s, st));
+  PSG_TRY(check_request_flags(s));
+  const int missing = s->flags_host[F_MISSING];
+  if (missing == 0) return PSG_OK;
+  PSG_TRY(insert_missing(s, q, n, (uint64_t)missing, st));
+  PSG_TRY(launch_resolve(s, q, n, s->slots2, st));
+  switch (s->dtype) {
+    case PSG_F32: PSG_TRY(run_fixup<PSG_F32>(s, op, vals, out, n, st)); break;
+    case PSG_F64: PSG_TRY(run_fixup<PSG_F64>(s, op, vals, out, n, st)); break;
+    case PSG_F16: PSG_TRY(run_fixup<PSG_F16>(s, op, vals, out, n, st)); break;
+    default: PSG_TRY(run_fixup<PSG_BF16>(s, op, vals, out, n, st)); break;
   }
+  PSG_TRY(read_flags(s, st));
+  PSG_REQUIRE(s->flags_host[F_MISSING] == 0, PSG_ERR_HIP, "SORTED store: keys still absent after insert");
+  return PSG_OK;
+}
+
+// Resolve q to slots (psg_store_resolve), inserting absent keys when asked.
+static int sorted_resolve(psg_store* s, const uint64_t* q, uint64_t n, bool insert, hipStream_t st) {
+  PSG_TRY(ensure_slots(s, n));
+  PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+  PSG_TRY(read_flags(s, st));
+  PSG_TRY(check_request_flags(s));
+  const int missing = s->flags_host[F_MISSING];
+  if (missing == 0 || !insert) return PSG_OK;
+  PSG_TRY(insert_missing(s, q, n, (uint64_t)missing, st));
+  PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+  PSG_TRY(read_flags(s, st));
+  PSG_REQUIRE(s->flags_host[F_MISSING] == 0, PSG_ERR_HIP, "SORTED store: keys still absent after insert");
   return PSG_OK;
 }
 
@@ -434,6 +554,8 @@ int psg_store_destroy(psg_store* s) {
   if (s->vals) (void)hipFree(s->vals);
   if (s->keys) (void)hipFree(s->keys);
   if (s->slots) (void)hipFree(s->slots);
+  if (s->slots2) (void)hipFree(s->slots2);
+  if (s->wlo) (void)hipFree(s->wlo);
   if (s->flags) (void)hipFree(s->flags);
   if (s->flags_host) (void)hipHostFree(s->flags_host);
   delete s;
@@ -499,11 +621,7 @@ int psg_store_handle(psg_store* s, int flags, const uint64_t* keys, uint64_t fir
   }
   // SORTED
   PSG_REQUIRE(keys, PSG_ERR_INVALID, "SORTED store needs explicit keys");
-  uint64_t base = UINT64_MAX;
-  PSG_TRY(sorted_resolve(s, keys, n, true, &base, st));
-  if (base != UINT64_MAX)
-    return dense_request(s->dtype, flags, (char*)s->vals + base * s->esize, vals, out, n, st);
-  return slot_request(s->dtype, flags, s->vals, s->slots, vals, out, n, st);
+  return sorted_request(s, flags, keys, vals, out, n, st);
 }
 
 int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert, uint32_t* slots,
@@ -523,7 +641,7 @@ int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert
     PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE, "key outside the DENSE store slots");
     return PSG_OK;
   }
-  PSG_TRY(sorted_resolve(s, keys, n, insert != 0, nullptr, st));
+  PSG_TRY(sorted_resolve(s, keys, n, insert != 0, st));
   PSG_HIP(hipMemcpyAsync(slots, s->slots, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return PSG_OK;
 }

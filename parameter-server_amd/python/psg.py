@@ -43,7 +43,7 @@ EXPORTS = [
     "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
-    "psg_comm_push_pull",
+    "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
     "psg_adam_create", "psg_adam_destroy", "psg_lr_apply",
 ]
 
@@ -110,6 +110,8 @@ def lib() -> C.CDLL:
             "psg_comm_push": ([vp, vp, vp, u64, vp, vp], i32),
             "psg_comm_pull": ([vp, vp, vp, u64, vp], i32),
             "psg_comm_push_pull": ([vp, vp, vp, vp, u64, i32, vp], i32),
+            "psg_comm_push_keyed": ([vp, vp, vp, vp, u64, vp, vp], i32),
+            "psg_comm_pull_keyed": ([vp, vp, vp, vp, u64, vp, vp], i32),
             "psg_adam_create": ([u64, f64, f64, f64, f64, C.POINTER(vp)], i32),
             "psg_adam_destroy": ([vp], i32),
             "psg_lr_apply": ([vp, vp, u64, f32, vp, i32, vp], i32),
@@ -353,6 +355,16 @@ class Comm:
     def push_pull(self, shard: Store, vals, out, n_total: int, nbuckets: int, stream=None) -> None:
         _call("psg_comm_push_pull", self.h, shard.h, _ptr(vals), _ptr(out), n_total, nbuckets,
               _s(stream))
+
+    def push_keyed(self, shard: Store, keys, vals, n: int, key_pos, stream=None) -> None:
+        kp = np.ascontiguousarray(key_pos, dtype=np.uint64)
+        _call("psg_comm_push_keyed", self.h, shard.h, _ptr(keys), _ptr(vals), n,
+              kp.ctypes.data_as(C.c_void_p), _s(stream))
+
+    def pull_keyed(self, shard: Store, keys, out, n: int, key_pos, stream=None) -> None:
+        kp = np.ascontiguousarray(key_pos, dtype=np.uint64)
+        _call("psg_comm_pull_keyed", self.h, shard.h, _ptr(keys), _ptr(out), n,
+              kp.ctypes.data_as(C.c_void_p), _s(stream))
 
     def close(self) -> None:
         if self.h.value:

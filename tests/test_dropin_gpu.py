@@ -66,6 +66,17 @@ def test_reference_benchmark_runs():
     assert "Push average time" in r.stdout and "Pull average time" in r.stdout
 
 
+@pytest.mark.parametrize("nw,sync,adam", [(1, 0, 0), (1, 0, 1), (3, 0, 0), (1, 1, 1)])
+def test_lr_server_in_hbm_matches_reference_update(nw, sync, adam):
+    """KVServerLRHandle (BSP merge + SGD/Adam on the GPU) vs a replay of
+    LRServer.h:151-189 / Adam.h:28-34, bit for bit (tests/harness/lr_sync_gpu.cpp)."""
+    exe = os.path.join(BIN, "lr_sync_gpu")
+    _need(exe)
+    r = run(exe, "-ns", 1, "-nw", nw, sync, adam, 3, 4, 123)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "matches the reference update" in r.stdout
+
+
 @pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
 def test_device_frames_end_to_end(ns, nw):
     exe = os.path.join(BIN, "kv_cluster_device")

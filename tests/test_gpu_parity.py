@@ -293,6 +293,30 @@ def test_lr_apply_bitexact(adam):
 
 
 @pytest.mark.parametrize("force", [False, True])
+def test_comm_keyed_single_rank(force, monkeypatch):
+    """Keyed BSP Push/Pull (grouped RCCL reduce / broadcast) into a SORTED shard."""
+    if force:
+        monkeypatch.setenv("PSG_COMM_FORCE_COLLECTIVE", "1")
+    c = psg.Comm(psg.comm_id(), 1, 0)
+    rng = np.random.default_rng(21)
+    keys = np.unique(rng.integers(0, KMAX, 200000, dtype=np.uint64))
+    n = len(keys)
+    v = rng.uniform(-1, 1, n).astype(np.float32)
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    dk, dv = dev(keys), dev(v)
+    b, e = psg.server_ranges(1)
+    kp, _ = psg.slice_keys(dk, n, b, e)
+    orc = oracle.Store()
+    out = psg.DeviceBuffer(n * 4)
+    for _ in range(3):
+        c.push_keyed(st, dk, dv, n, kp)
+        orc.handle(oracle.PUSH, keys, v, n)
+    c.pull_keyed(st, dk, out, n, kp)
+    np.testing.assert_array_equal(out.download(np.float32, n), orc.handle(oracle.PULL, keys, None, n))
+    c.close()
+
+
+@pytest.mark.parametrize("force", [False, True])
 @pytest.mark.parametrize("dtype,n", [(psg.F32, 1 << 20), (psg.F32, 1000003), (psg.F16, 65600)])
 def test_comm_single_rank_push_pull(force, dtype, n, monkeypatch):
     """force=True runs the RCCL reduce-scatter / all-gather and the pipelined
