@@ -71,13 +71,19 @@ __device__ __forceinline__ uint32_t lower_bound_lds(const uint64_t* a, uint32_t 
 }
 
 // Pass 2: resolve sorted request keys q[0..n) against K[0..S).  Each block
-// stages its tile's window of K into LDS with coalesced loads and binary-
-// searches there (a global search only when a sparse request leaves a window
-// wider than kWin).  slots[i] = index of q[i] in K, or kNoSlot.  flags:
-// [F_MISSING] += absent keys, [F_NONCONTIG] |= slots not equal to base + i,
-// [F_RANGE] |= key outside [kb, ke), [F_UNSORTED] |= q not strictly ascending.
-// A slot is only written when K[slot] == key, so unsorted input never
-// produces a wrong slot (it is flagged and the request rejected).
+// stages its tile's window of K into LDS with coalesced loads; every lane then
+// owns 4 consecutive request keys: one LDS binary search places the first,
+// and each next key (larger, since q is ascending) is placed by a merge walk —
+// it is almost always at the previous position or the one after, two LDS
+// reads — with a binary search of the rest of the window as the fallback.  A
+// global search is used only when a sparse request leaves a window wider than
+// kWin.  slots[i] = index of q[i] in K, or kNoSlot.  flags: [F_MISSING] +=
+// absent keys, [F_NONCONTIG] |= slots not equal to base + i, [F_RANGE] |= key
+// outside [kb, ke), [F_UNSORTED] |= q not strictly ascending.  A slot is only
+// written when K[slot] == key, so unsorted input never produces a wrong slot
+// (it is flagged and the request rejected).
+constexpr int kPerLane = kTile / kBlock;  // 4 consecutive keys per lane
+
 __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q, uint64_t n,
                                                  const uint64_t* __restrict__ K, uint64_t S,
                                                  const uint64_t* __restrict__ wlo, uint64_t kb,
@@ -99,23 +105,45 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
     if (staged)
       for (uint64_t j = threadIdx.x; j < W; j += kBlock) sK[j] = K[lo + j];
     __syncthreads();
-    for (uint64_t i = t0 + threadIdx.x; i < t1; i += kBlock) {
+    const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
+    uint64_t prev = i0 > 0 && i0 < t1 ? q[i0 - 1] : 0;
+    uint32_t r = 0;  // lower bound of the previous key inside the window
+    uint32_t out[kPerLane];
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      const uint64_t i = i0 + k;
+      out[k] = kNoSlot;
+      if (i >= t1) continue;
       const uint64_t key = q[i];
       if (key < kb || key >= ke) range = 1;
-      if (i > 0 && q[i - 1] >= key) unsorted = 1;
+      if (i > 0 && prev >= key) unsorted = 1;
+      prev = key;
       uint64_t p;
       bool found;
       if (staged) {
-        const uint32_t r = lower_bound_lds(sK, (uint32_t)W, key);
+        const uint32_t w = (uint32_t)W;
+        if (k == 0) {
+          r = lower_bound_lds(sK, w, key);
+        } else if (!(r < w && sK[r] >= key)) {
+          if (r + 1 < w && sK[r + 1] >= key) r = r + 1;  // the next store key
+          else r = (r + 1 >= w) ? w : r + 1 + lower_bound_lds(sK + r + 1, w - r - 1, key);
+        }
         p = lo + r;
-        found = r < W && sK[r] == key;
+        found = r < w && sK[r] == key;
       } else {
         p = lower_bound_dev(K, lo, hi, key);
         found = p < S && K[p] == key;
       }
-      slots[i] = found ? (uint32_t)p : kNoSlot;
+      out[k] = found ? (uint32_t)p : kNoSlot;
       if (!found) missing++;
       if (!found || p != base + i) noncontig = 1;
+    }
+    if (i0 + kPerLane <= t1 && ((i0 & 3) == 0)) {
+      // 16-B store of the lane's 4 slots (slots is our own 256-B aligned buffer)
+      *reinterpret_cast<u32x4*>(slots + i0) = u32x4{out[0], out[1], out[2], out[3]};
+    } else {
+      for (int k = 0; k < kPerLane; ++k)
+        if (i0 + k < t1) slots[i0 + k] = out[k];
     }
     __syncthreads();
   }

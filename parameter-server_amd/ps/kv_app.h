@@ -78,6 +78,16 @@ SVector<T> ToDevice(const SVector<T>& v, int dev) {
   device::CopySync(d.data(), v.data(), v.size() * sizeof(T), 0);
   return d;
 }
+/* the same, enqueued on the thread stream without waiting (the caller's
+ * later work on that stream is ordered after it; keep `v` alive until then) */
+template <typename T>
+SVector<T> ToDeviceAsync(const SVector<T>& v, int dev) {
+  if (v.on_device() || v.empty()) return v;
+  SVector<T> d = SVector<T>::OnDevice(v.size(), dev);
+  device::Check(psg_memcpy(d.data(), v.data(), v.size() * sizeof(T), 0, device::ThreadStream()),
+                "psg_memcpy H2D");
+  return d;
+}
 }  // namespace detail
 
 template <typename Value>
@@ -227,19 +237,14 @@ class KVServer : public SimpleApp {
   /* a host handle: sees host frames (KVApp.h:405-408) */
   void SetRequestHandle(const ReqHandle& request_handle) {
     CHECK(static_cast<bool>(request_handle)) << "invalid request handle";
-    request_handle_ = request_handle;
-    device_frames_ = false;
+    Install(request_handle, false);
   }
   /* the default handle keeps its store in HBM and takes frames where they are */
-  void SetRequestHandle(const KVServerDefaultHandle<Value>& h) {
-    request_handle_ = h;
-    device_frames_ = true;
-  }
+  void SetRequestHandle(const KVServerDefaultHandle<Value>& h) { Install(h, true); }
   /* a handle that consumes HBM frames itself */
   void SetDeviceRequestHandle(const ReqHandle& request_handle) {
     CHECK(static_cast<bool>(request_handle)) << "invalid request handle";
-    request_handle_ = request_handle;
-    device_frames_ = true;
+    Install(request_handle, true);
   }
 
   /* reply to a request (KVApp.h:491-513); frames may be host or HBM */
@@ -247,8 +252,21 @@ class KVServer : public SimpleApp {
 
  private:
   void OnReceive(const Message& msg) override;
+  void Install(const ReqHandle& h, bool device_frames) {
+    {
+      std::lock_guard<std::mutex> lk(handle_mu_);
+      request_handle_ = h;
+      device_frames_ = device_frames;
+    }
+    handle_cv_.notify_all();
+  }
+  // The customer thread may receive a request before the program installs its
+  // handle (it is created with the KVServer); it waits for the handle instead
+  // of failing the reference's CHECK (KVApp.h:487) on that race.
   ReqHandle request_handle_;
   bool device_frames_ = false;
+  std::mutex handle_mu_;
+  std::condition_variable handle_cv_;
 };
 
 /* The default handle (KVApp.h:433-458): `store[key] += val` for a push,
@@ -279,9 +297,9 @@ struct KVServerDefaultHandle {
     const int flags = (req_meta.push ? PSG_PUSH : 0) | (req_meta.pull ? PSG_PULL : 0);
     SVector<Value> dout;
     if (n && flags) {
-      SVector<Key> dkeys = detail::ToDevice(req_data.keys, dev);
+      SVector<Key> dkeys = detail::ToDeviceAsync(req_data.keys, dev);
       SVector<Value> dvals;
-      if (req_meta.push) dvals = detail::ToDevice(req_data.vals, dev);
+      if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
       if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
       psg_stream s = device::ThreadStream();
       device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
@@ -325,6 +343,14 @@ void KVServer<Value>::OnReceive(const Message& msg) {
   meta.sender = msg.meta.sender;
   meta.timestamp = msg.meta.timestamp;
   meta.customer_id = msg.meta.customer_id;
+  bool device_frames, installed;
+  {
+    std::unique_lock<std::mutex> lk(handle_mu_);
+    handle_cv_.wait_for(lk, std::chrono::seconds(30), [this] { return static_cast<bool>(request_handle_); });
+    installed = static_cast<bool>(request_handle_);
+    device_frames = device_frames_;
+  }
+  CHECK(installed) << "no request handle installed 30 s after the first request";
   KVPairs<Value> data;
   const size_t n = msg.data.size();
   if (n) {
@@ -336,13 +362,13 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       data.lens = msg.data[2];
       CHECK_EQ(data.lens.size(), data.keys.size());
     }
-    if (!device_frames_) {
+    if (!device_frames) {
       data.keys = detail::ToHost(data.keys);
       data.vals = detail::ToHost(data.vals);
       data.lens = detail::ToHost(data.lens);
     }
   }
-  CHECK(static_cast<bool>(request_handle_));
+  // called in place: a handle keeps its state across requests (KVApp.h:457)
   request_handle_(meta, data, this);
 }
 

@@ -30,6 +30,8 @@ namespace ps {
 namespace device {
 // Pooled HBM allocation on `device` (implemented in src/device.cc).
 std::shared_ptr<void> Alloc(size_t bytes, int device);
+// Pooled pinned host block for a large host array, or nullptr (use the heap).
+std::shared_ptr<void> HostAlloc(size_t bytes);
 }  // namespace device
 
 template <typename T>
@@ -138,7 +140,11 @@ class SVector {
   void reserve(size_t n) {
     if (n <= capacity_) return;
     CHECK(!on_device()) << "reserve on a device SVector";
-    std::shared_ptr<T> np(new T[n](), [](T* p) { delete[] p; });
+    std::shared_ptr<T> np;
+    if (auto pinned = device::HostAlloc(n * sizeof(T)))  // large frames: pinned, PCIe-rate copies
+      np = std::shared_ptr<T>(pinned, static_cast<T*>(pinned.get()));
+    else
+      np = std::shared_ptr<T>(new T[n](), [](T* p) { delete[] p; });
     if (size_) std::memcpy(np.get(), data(), size_ * sizeof(T));
     ptr_ = np;
     capacity_ = n;

@@ -97,6 +97,35 @@ std::shared_ptr<void> Alloc(size_t bytes, int dev) {
   });
 }
 
+// Pinned host blocks for large host arrays (>= 1 MiB): H2D / D2H of request
+// and reply frames then run at PCIe rate without the runtime's pageable
+// staging.  Pooled like the HBM blocks (device key -1).  Off without a GPU
+// or with PS_PINNED_HOST=0.
+std::shared_ptr<void> HostAlloc(size_t bytes) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("PS_PINNED_HOST");
+    return Count() > 0 && !(e && std::atoi(e) == 0);
+  }();
+  if (!enabled || bytes < (1u << 20)) return nullptr;
+  Pool& pool = GlobalPool();
+  const size_t rb = Pool::Round(bytes);
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    auto& fl = pool.free[{-1, rb}];
+    if (!fl.empty()) {
+      p = fl.back();
+      fl.pop_back();
+    }
+  }
+  if (!p && psg_host_alloc(&p, rb) != PSG_OK) return nullptr;  // fall back to pageable memory
+  return std::shared_ptr<void>(p, [rb](void* q) {
+    Pool& pl = GlobalPool();
+    std::lock_guard<std::mutex> lk(pl.mu);
+    pl.free[{-1, rb}].push_back(q);
+  });
+}
+
 void EnableAllPeerAccess() {
   const int n = Count();
   for (int a = 0; a < n; ++a)
