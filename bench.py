@@ -420,6 +420,10 @@ def main(argv=None) -> None:
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.barrier()
+    if backend.comm is not None:
+        backend.sync()
+        backend.comm.close()
+    if dist is not None:
         dist.destroy_process_group()
 
 

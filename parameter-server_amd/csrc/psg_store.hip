@@ -40,22 +40,44 @@ __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__
   return lo;
 }
 
-constexpr int kWin = 4096;  // LDS-staged window of store keys (32 KiB)
+constexpr int kWin = 2048;  // LDS-staged window of store keys (16 KiB: 10 blocks per CU)
 
-// Pass 1: the store-key window of every 1024-key request tile, one lane per
-// tile (all searches in flight at once instead of two per block in turn):
-// wlo[t] = lower_bound(K, q[t * kTile]); wlo[ntiles] = lower_bound(K, q[n-1]) + 1.
+// lower_bound by one wave: 64 lanes probe 64 evenly spaced keys per round and
+// a ballot brackets the answer, so a 10 M-key store takes 4 rounds of one
+// parallel load instead of 24 dependent loads.  Wave-uniform result.
+__device__ __forceinline__ uint64_t lower_bound_wave(const uint64_t* __restrict__ a, uint64_t S,
+                                                     uint64_t key) {
+  const int lane = threadIdx.x & 63;
+  uint64_t lo = 0, hi = S;  // the answer is in [lo, hi]
+  while (hi - lo > 64) {
+    const uint64_t step = (hi - lo + 63) / 64;
+    const uint64_t p = lo + (uint64_t)lane * step;
+    const bool pred = p < hi && a[p] < key;
+    const uint64_t c = (uint64_t)__popcll(__ballot(pred));
+    if (c == 0) return lo;
+    const uint64_t pc = lo + c * step;
+    lo = lo + (c - 1) * step + 1;
+    hi = pc < hi ? pc : hi;
+  }
+  const uint64_t p = lo + (uint64_t)lane;
+  const bool pred = p < hi && a[p] < key;
+  return lo + (uint64_t)__popcll(__ballot(pred));
+}
+
+// Pass 1: the store-key window of every 1024-key request tile, one wave per
+// tile: wlo[t] = lower_bound(K, q[t * kTile]); wlo[ntiles] = lower_bound(K, q[n-1]) + 1.
 __global__ __launch_bounds__(256) void k_tile_windows(const uint64_t* __restrict__ q, uint64_t n,
                                                       const uint64_t* __restrict__ K, uint64_t S,
                                                       uint64_t* __restrict__ wlo) {
   const uint64_t ntiles = (n + kTile - 1) / kTile;
-  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t <= ntiles;
-       t += (uint64_t)gridDim.x * kBlock) {
+  const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
+  for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t <= ntiles; t += waves) {
     if (t < ntiles) {
-      wlo[t] = lower_bound_dev(K, 0, S, q[t * kTile]);
+      const uint64_t r = lower_bound_wave(K, S, q[t * kTile]);
+      if ((threadIdx.x & 63) == 0) wlo[t] = r;
     } else {
-      const uint64_t h = lower_bound_dev(K, 0, S, q[n - 1]);
-      wlo[t] = h < S ? h + 1 : S;
+      const uint64_t h = lower_bound_wave(K, S, q[n - 1]);
+      if ((threadIdx.x & 63) == 0) wlo[t] = h < S ? h + 1 : S;
     }
   }
 }
@@ -339,7 +361,7 @@ static int launch_resolve(psg_store* s, const uint64_t* q, uint64_t n, uint32_t*
                           hipStream_t st) {
   const uint64_t ntiles = (n + kTile - 1) / kTile;
   PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
-  k_tile_windows<<<grid_n(ntiles + 1, kBlock), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
+  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
   k_resolve<<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
                                                   s->key_end, slots, s->flags);
   PSG_HIP(hipGetLastError());

