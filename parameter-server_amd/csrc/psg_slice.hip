@@ -11,6 +11,8 @@
 // 24 dependent loads.  With lens, the value bound of each slice is a per-slice
 // sum of lens (KVApp.h:565-569), done as a 2-D grid of chunk partial sums.
 #include <algorithm>
+#include <cstring>
+#include <map>
 #include <vector>
 
 #include "psg_internal.h"
@@ -93,6 +95,36 @@ static void launch_merge(const SegTable& t, int nseg, uint64_t maxcount, char* d
   k_merge_copy<W><<<dim3((unsigned)bx, (unsigned)nseg), kBlock, 0, st>>>(t, dst);
 }
 
+// Per-thread, per-GPU scratch of the slicer: the bounds / length sums in HBM
+// and pinned mirrors, so a request costs no allocation (a worker slices every
+// Push and Pull).  Kept for the thread's lifetime.
+struct SliceScratch {
+  uint64_t* pos_dev = nullptr;
+  unsigned long long* sums_dev = nullptr;
+  uint64_t* pos_host = nullptr;
+  int cap = 0;
+};
+static thread_local std::map<int, SliceScratch> t_slice_scratch;
+
+static int get_slice_scratch(int nb, SliceScratch** out) {
+  int dev = 0;
+  PSG_HIP(hipGetDevice(&dev));
+  SliceScratch& s = t_slice_scratch[dev];
+  if (s.cap < nb) {
+    if (s.pos_dev) (void)hipFree(s.pos_dev);
+    if (s.sums_dev) (void)hipFree(s.sums_dev);
+    if (s.pos_host) (void)hipHostFree(s.pos_host);
+    s = SliceScratch();
+    const int cap = std::max(nb, 64);
+    PSG_HIP(hipMalloc((void**)&s.pos_dev, cap * sizeof(uint64_t)));
+    PSG_HIP(hipMalloc((void**)&s.sums_dev, cap * sizeof(unsigned long long)));
+    PSG_HIP(hipHostMalloc((void**)&s.pos_host, cap * sizeof(uint64_t), hipHostMallocDefault));
+    s.cap = cap;
+  }
+  *out = &s;
+  return PSG_OK;
+}
+
 }  // namespace psg
 
 using namespace psg;
@@ -134,9 +166,10 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
                 (unsigned long long)num_vals, (unsigned long long)n);
   }
   hipStream_t st = (hipStream_t)stream;
-  uint64_t* pos_dev = nullptr;
-  unsigned long long* sums_dev = nullptr;
-  PSG_HIP(hipMalloc((void**)&pos_dev, nb * sizeof(uint64_t)));
+  SliceScratch* sc = nullptr;
+  PSG_TRY(get_slice_scratch(nb, &sc));
+  uint64_t* pos_dev = sc->pos_dev;
+  unsigned long long* sums_dev = sc->sums_dev;
   int rc = PSG_OK;
   for (int b0 = 0; b0 < nb; b0 += kMaxTargets) {
     Targets t;
@@ -148,8 +181,9 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
     k_bounds<<<cnt, kBlock, 0, st>>>(keys, n, t, pos_dev + b0);
   }
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpyAsync(key_pos_host, pos_dev, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(sc->pos_host, pos_dev, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) memcpy(key_pos_host, sc->pos_host, nb * sizeof(uint64_t));
   if (e != hipSuccess) {
     rc = hip_fail(e, "psg_slice bounds", __FILE__, __LINE__);
   } else if (key_pos_host[num_servers] != n) {
@@ -166,8 +200,7 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
       uint64_t maxseg = 0;
       for (int i = 0; i < num_servers; ++i)
         maxseg = std::max<uint64_t>(maxseg, key_pos_host[i + 1] - key_pos_host[i]);
-      e = hipMalloc((void**)&sums_dev, num_servers * sizeof(unsigned long long));
-      if (e == hipSuccess) e = hipMemsetAsync(sums_dev, 0, num_servers * sizeof(unsigned long long), st);
+      e = hipMemsetAsync(sums_dev, 0, num_servers * sizeof(unsigned long long), st);
       if (e == hipSuccess && maxseg > 0) {
         dim3 g((unsigned)((maxseg + kLenChunk - 1) / kLenChunk), (unsigned)num_servers);
         k_seg_len_sum<<<g, kBlock, 0, st>>>(lens, pos_dev, sums_dev);
@@ -187,8 +220,6 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
       }
     }
   }
-  (void)hipFree(pos_dev);
-  if (sums_dev) (void)hipFree(sums_dev);
   return rc;
 }
 
