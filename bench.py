@@ -65,6 +65,8 @@ class GpuBackend:
         psg.set_device(local_rank)
         self.stream = psg.Stream()
         self.comm = None
+        self.xgmi = None
+        self.mode = "rccl"  # "rccl" (RS + AG, or pipelined when fused) or "xgmi"
         self.fused = False
         self.nbuckets = 1
 
@@ -95,7 +97,35 @@ class GpuBackend:
             self.dist.broadcast_object_list(uid, src=0)
             self.comm = p.Comm(uid[0], self.world, self.rank)
             self.scratch = p.DeviceBuffer(blk * self.vb)
+            if not self.keyed:
+                self._setup_xgmi()
         self.sync()
+
+    def _setup_xgmi(self):
+        """Map every peer's request vector and shard (hipIpc) for the one-shot
+        xGMI exchange (psg_xgmi_push / _pull); a node barrier orders the phases."""
+        import uuid
+        p = self.p
+        self.xgmi = None
+        sptr = self.store.info().vals
+        mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr))
+        allh = [None] * self.world
+        self.dist.all_gather_object(allh, mine)
+        tag = [uuid.uuid4().hex[:16] if self.rank == 0 else None]
+        self.dist.broadcast_object_list(tag, src=0)
+        self._peer_ptrs = []
+        vptrs, sptrs = [], []
+        for r in range(self.world):
+            if r == self.rank:
+                vptrs.append(self.vals.ptr)
+                sptrs.append(sptr)
+            else:
+                vptrs.append(p.ipc_open(allh[r][0]))
+                sptrs.append(p.ipc_open(allh[r][1]))
+                self._peer_ptrs += [vptrs[-1], sptrs[-1]]
+        self.xgmi = p.Xgmi(self.world, self.rank, vptrs, sptrs)
+        self.node_barrier = p.NodeBarrier("psg_bench_" + tag[0], self.world, self.rank)
+        self.node_barrier.wait()
 
     def _key_pos(self):
         # the worker's DefaultSlicer on its HBM keys (psg_slice), every request
@@ -107,6 +137,11 @@ class GpuBackend:
 
     # -- one phase at a time (N = 1, or the sequential RS / AG at N > 1)
     def push(self):
+        if self.mode == "xgmi":
+            self.xgmi.push(self.store, self.L, self.stream)
+            self.stream.sync()
+            self.node_barrier.wait()
+            return
         if self.keyed:
             kp = self._key_pos()
             if self.comm is None:
@@ -120,6 +155,11 @@ class GpuBackend:
             self.comm.push(self.store, self.vals, self.L, self.scratch, self.stream)
 
     def pull(self):
+        if self.mode == "xgmi":
+            self.xgmi.pull(self.store, self.out, self.L, self.stream)
+            self.stream.sync()
+            self.node_barrier.wait()
+            return
         if self.keyed:
             kp = self._key_pos()
             if self.comm is None:
@@ -136,32 +176,48 @@ class GpuBackend:
     def step(self):
         self.comm.push_pull(self.store, self.vals, self.out, self.L, self.nbuckets, self.stream)
 
+    def _set_mode(self, cand):
+        mode, nb = cand
+        self.mode, self.nbuckets = mode, nb
+        self.fused = mode == "rccl" and nb > 1
+
     def calibrate(self, dist, iters=3):
-        """Pick sequential RS+AG (nbuckets 1) or a pipelined bucket count by timing
-        each a few times; the max over ranks decides, so every rank picks the same."""
+        """Pick the exchange for this node by timing each candidate a few times
+        (wall clock, barrier-synced): RCCL reduce-scatter then all-gather, the
+        RCCL pipelined over 4/8/16 buckets, or the one-shot xGMI kernels.  The
+        max over ranks decides, so every rank picks the same."""
         if self.comm is None or self.keyed:
             return
         import torch
-        cands = [1, 4, 8, 16]
+        cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)]
+        if self.xgmi is not None:
+            cands.append(("xgmi", 0))
         times = []
-        for nb in cands:
-            self.nbuckets = nb
-            self.step()
+        for cand in cands:
+            self._set_mode(cand)
+            self._one_step()
             self.sync()
-            a, b = self.new_event(), self.new_event()
-            self.record(a)
+            dist.barrier()
+            t0 = time.perf_counter()
             for _ in range(iters):
-                self.step()
-            self.record(b)
+                self._one_step()
             self.sync()
-            times.append(self.elapsed(a, b) / iters)
+            times.append((time.perf_counter() - t0) * 1e3 / iters)
+            dist.barrier()
         t = torch.tensor(times, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         best = int(t.argmin().item())
-        self.nbuckets = cands[best]
-        self.fused = self.nbuckets > 1
-        self.calibration = {str(c): round(x, 4) for c, x in zip(cands, t.tolist())}
+        self._set_mode(cands[best])
+        self.calibration = {f"{m}{'' if m == 'xgmi' else '/' + str(nb)}": round(x, 4)
+                            for (m, nb), x in zip(cands, t.tolist())}
         self.pushes_in_calibration = len(cands) * (iters + 1)
+
+    def _one_step(self):
+        if self.fused:
+            self.step()
+        else:
+            self.push()
+            self.pull()
 
     def new_event(self):
         return self.p.Event()
@@ -308,8 +364,13 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         "parity_check": ok,
     }
     if world > 1 and hasattr(backend, "nbuckets"):
-        res["config"]["exchange"] = ("pipelined reduce/broadcast, %d buckets" % backend.nbuckets
-                                     if fused else "reduce-scatter then all-gather")
+        if getattr(backend, "mode", "rccl") == "xgmi":
+            res["config"]["exchange"] = "one-shot xGMI kernels (psg_xgmi push/pull, peers via hipIpc)"
+        elif getattr(backend, "keyed", False):
+            res["config"]["exchange"] = "RCCL grouped reduce / broadcast of the key-range segments"
+        else:
+            res["config"]["exchange"] = ("RCCL pipelined reduce/broadcast, %d buckets" % backend.nbuckets
+                                         if fused else "RCCL reduce-scatter then all-gather")
         res["config"]["calibration_ms"] = getattr(backend, "calibration", None)
     if world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
@@ -420,6 +481,13 @@ def main(argv=None) -> None:
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.barrier()
+    if backend.xgmi is not None:
+        backend.sync()
+        backend.node_barrier.wait()  # no peer still reads a buffer this rank unmaps
+        backend.xgmi.close()
+        for ptr in backend._peer_ptrs:
+            backend.p.ipc_close(ptr)
+        backend.node_barrier.close()
     if backend.comm is not None:
         backend.sync()
         backend.comm.close()

@@ -260,6 +260,32 @@ int psg_comm_push_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, con
 int psg_comm_pull_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, void* out,
                         uint64_t n, const uint64_t* key_pos_host, psg_stream stream);
 
+/* ---- one-shot xGMI exchange (no RCCL) -------------------------------------
+ * Every rank maps its peers' request vectors and store shards (hipIpc handles
+ * the caller exchanges: psg_ipc_export on the owner, psg_ipc_open on the
+ * others) and reads all peers in ONE kernel, so the 7 xGMI links of an MI355X
+ * carry traffic together and the reduction is fused with the accumulate.
+ * Ordering between ranks is the caller's (psg_node_barrier after each phase). */
+typedef struct psg_xgmi psg_xgmi;
+typedef struct psg_barrier psg_barrier;
+int psg_ipc_handle_bytes(void);
+int psg_ipc_export(const void* dptr, void* handle_out);   /* dptr: start of an allocation */
+int psg_ipc_open(const void* handle, void** dptr_out);
+int psg_ipc_close(void* dptr);
+/* peer_vals[r] / peer_stores[r]: rank r's request vector (n_total values) and
+ * DENSE shard value array, as pointers valid in this process. */
+int psg_xgmi_create(int nranks, int rank, void* const* peer_vals, void* const* peer_stores,
+                    psg_xgmi** out);
+int psg_xgmi_destroy(psg_xgmi* x);
+/* shard += sum over ranks w (in rank order) of vals_w[block r] */
+int psg_xgmi_push(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream);
+/* out[w * blk ...] = shard of rank w, for every w */
+int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream);
+/* Host barrier of the ranks of one node over a POSIX shared-memory page. */
+int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier** out);
+int psg_node_barrier_wait(psg_barrier* b, double timeout_s);
+int psg_node_barrier_destroy(psg_barrier* b);
+
 /* ======================================================================== */
 /* LR server apply                                             */
 /* ======================================================================== */

@@ -1,0 +1,241 @@
+// psg_xgmi.hip — one-shot BSP exchange over xGMI without RCCL.
+//
+// MI355X links every GPU of a node to every other GPU (7 xGMI links per GPU).
+// A ring collective moves each byte over one link per step; here every rank
+// maps its peers' buffers (hipIpc handles, exchanged by the caller) and
+// touches all of them in ONE kernel, so all 7 links carry traffic at once and
+// the reduction is fused with the store update:
+//
+//   Push (psg_xgmi_push)  rank r:  shard[i] = ((shard[i] + v_0[r*blk+i]) + v_1[..]) + ...
+//                         summed in rank order 0..N-1 (deterministic), reading
+//                         N-1 peers' request vectors in place — the
+//                         reduce-scatter and the accumulate of psg_comm_push in
+//                         one pass over HBM.
+//   Pull (psg_xgmi_pull)  rank r:  out[w*blk + i] = shard_w[i] for every w —
+//                         the all-gather, reading N-1 peers' shards in place.
+//
+// Ordering between ranks is the caller's: all Pushes must be complete before
+// any Pull reads a shard, and every Pull complete before the next Push
+// changes a shard (a node barrier after each phase; psg_node_barrier is one).
+// Per-rank traffic: Push reads (N-1)/N of its block from peers; Pull reads
+// (N-1)/N of the vector — the same bytes as RS + AG, in one hop each.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstring>
+#include <string>
+
+#include "psg_internal.h"
+
+namespace psg {
+
+constexpr int kMaxPeers = 16;
+
+struct Peers {
+  const u32x4* p[kMaxPeers];
+};
+
+// store += sum_w src_w (16-B vectors), sources added in rank order.
+template <int DT>
+__global__ __launch_bounds__(256) void k_xgmi_push(u32x4* __restrict__ store, Peers src, int nsrc,
+                                                   uint64_t nvec) {
+  using E = Elem<DT>;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nvec;
+       j += (uint64_t)gridDim.x * kBlock) {
+    u32x4 v[kMaxPeers];
+#pragma unroll
+    for (int w = 0; w < kMaxPeers; ++w)
+      if (w < nsrc) v[w] = __builtin_nontemporal_load(src.p[w] + j);
+    u32x4 acc = store[j];
+#pragma unroll
+    for (int w = 0; w < kMaxPeers; ++w)
+      if (w < nsrc) acc = E::add(acc, v[w]);
+    store[j] = acc;
+  }
+}
+
+// out[w*blk ...] = shard_w (16-B vectors); blockIdx.y = w.
+__global__ __launch_bounds__(256) void k_xgmi_pull(u32x4* __restrict__ out, Peers shard, uint64_t nvec) {
+  const int w = blockIdx.y;
+  const u32x4* __restrict__ s = shard.p[w];
+  u32x4* __restrict__ o = out + (uint64_t)w * nvec;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nvec;
+       j += (uint64_t)gridDim.x * kBlock)
+    __builtin_nontemporal_store(s[j], o + j);
+}
+
+}  // namespace psg
+
+struct psg_xgmi {
+  int nranks, rank;
+  void* vals[psg::kMaxPeers];
+  void* stores[psg::kMaxPeers];
+};
+
+struct psg_barrier {
+  struct Shared {
+    std::atomic<int> count;
+    std::atomic<int> generation;
+    int nranks;
+  };
+  Shared* sh;
+  int nranks, rank;
+  std::string name;
+};
+
+using namespace psg;
+
+extern "C" {
+
+int psg_ipc_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+int psg_ipc_export(const void* dptr, void* handle_out) {
+  PSG_REQUIRE(dptr && handle_out, PSG_ERR_INVALID, "psg_ipc_export: null argument");
+  hipIpcMemHandle_t h;
+  PSG_HIP(hipIpcGetMemHandle(&h, const_cast<void*>(dptr)));
+  memcpy(handle_out, &h, sizeof(h));
+  return PSG_OK;
+}
+
+int psg_ipc_open(const void* handle, void** dptr_out) {
+  PSG_REQUIRE(handle && dptr_out, PSG_ERR_INVALID, "psg_ipc_open: null argument");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  PSG_HIP(hipIpcOpenMemHandle(dptr_out, h, hipIpcMemLazyEnablePeerAccess));
+  return PSG_OK;
+}
+
+int psg_ipc_close(void* dptr) {
+  if (dptr) PSG_HIP(hipIpcCloseMemHandle(dptr));
+  return PSG_OK;
+}
+
+int psg_xgmi_create(int nranks, int rank, void* const* peer_vals, void* const* peer_stores,
+                    psg_xgmi** out) {
+  PSG_REQUIRE(out && peer_vals && peer_stores && nranks > 0 && nranks <= kMaxPeers && rank >= 0 &&
+                  rank < nranks,
+              PSG_ERR_INVALID, "psg_xgmi_create: bad arguments (at most %d ranks)", kMaxPeers);
+  psg_xgmi* x = new psg_xgmi();
+  memset(x, 0, sizeof(*x));
+  x->nranks = nranks;
+  x->rank = rank;
+  for (int r = 0; r < nranks; ++r) {
+    PSG_REQUIRE(peer_vals[r] && peer_stores[r], PSG_ERR_INVALID, "psg_xgmi_create: null peer %d", r);
+    PSG_REQUIRE(aligned16(peer_vals[r]) && aligned16(peer_stores[r]), PSG_ERR_INVALID,
+                "psg_xgmi_create: peer %d buffers not 16-B aligned", r);
+    x->vals[r] = peer_vals[r];
+    x->stores[r] = peer_stores[r];
+  }
+  *out = x;
+  return PSG_OK;
+}
+
+int psg_xgmi_destroy(psg_xgmi* x) {
+  delete x;
+  return PSG_OK;
+}
+
+int psg_xgmi_push(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream) {
+  PSG_REQUIRE(x && shard && shard->kind == PSG_STORE_DENSE, PSG_ERR_INVALID,
+              "psg_xgmi_push: need a DENSE shard");
+  PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_push: n_total %% nranks");
+  const uint64_t blk = n_total / (uint64_t)x->nranks;
+  PSG_REQUIRE(shard->capacity >= blk, PSG_ERR_RANGE, "psg_xgmi_push: shard too small");
+  PSG_REQUIRE(shard->vals == x->stores[x->rank], PSG_ERR_INVALID, "psg_xgmi_push: shard is not this rank's store");
+  const int es = shard->esize;
+  PSG_REQUIRE((blk * es) % 16 == 0, PSG_ERR_INVALID, "psg_xgmi_push: block must be a multiple of 16 B");
+  const uint64_t nvec = blk * es / 16;
+  if (nvec == 0) return PSG_OK;
+  Peers src;
+  for (int w = 0; w < x->nranks; ++w)
+    src.p[w] = (const u32x4*)((const char*)x->vals[w] + (uint64_t)x->rank * blk * es);
+  uint64_t g = (nvec + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 4;  // 2 per CU
+  if (g > cap) g = cap;
+  hipStream_t st = (hipStream_t)stream;
+  switch (shard->dtype) {
+    case PSG_F32: k_xgmi_push<PSG_F32><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
+    case PSG_F64: k_xgmi_push<PSG_F64><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
+    case PSG_F16: k_xgmi_push<PSG_F16><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
+    default: k_xgmi_push<PSG_BF16><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream) {
+  PSG_REQUIRE(x && shard && out, PSG_ERR_INVALID, "psg_xgmi_pull: null argument");
+  PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_pull: n_total %% nranks");
+  const int es = shard->esize;
+  const uint64_t blk = n_total / (uint64_t)x->nranks;
+  PSG_REQUIRE((blk * es) % 16 == 0 && aligned16(out), PSG_ERR_INVALID,
+              "psg_xgmi_pull: blocks and out must be 16-B aligned");
+  const uint64_t nvec = blk * es / 16;
+  if (nvec == 0) return PSG_OK;
+  Peers sh;
+  for (int w = 0; w < x->nranks; ++w) sh.p[w] = (const u32x4*)x->stores[w];
+  uint64_t gx = (nvec + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 4 / (uint64_t)x->nranks + 1;
+  if (gx > cap) gx = cap;
+  k_xgmi_pull<<<dim3((unsigned)gx, (unsigned)x->nranks), kBlock, 0, (hipStream_t)stream>>>((u32x4*)out, sh, nvec);
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+// ---- node barrier: a sense-counting barrier in a POSIX shared-memory page --
+int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier** out) {
+  PSG_REQUIRE(name && out && nranks > 0 && rank >= 0 && rank < nranks, PSG_ERR_INVALID,
+              "psg_node_barrier_create: bad arguments");
+  std::string nm = std::string("/") + name;
+  int fd = shm_open(nm.c_str(), O_CREAT | O_RDWR, 0600);
+  PSG_REQUIRE(fd >= 0, PSG_ERR_INVALID, "shm_open(%s) failed", nm.c_str());
+  if (ftruncate(fd, 4096) != 0) {
+    close(fd);
+    set_error("ftruncate(%s) failed", nm.c_str());
+    return PSG_ERR_INVALID;
+  }
+  void* p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  PSG_REQUIRE(p != MAP_FAILED, PSG_ERR_INVALID, "mmap(%s) failed", nm.c_str());
+  psg_barrier* b = new psg_barrier();
+  b->sh = (psg_barrier::Shared*)p;  // zero-filled on creation: count 0, generation 0
+  b->nranks = nranks;
+  b->rank = rank;
+  b->name = nm;
+  *out = b;
+  return PSG_OK;
+}
+
+int psg_node_barrier_wait(psg_barrier* b, double timeout_s) {
+  PSG_REQUIRE(b, PSG_ERR_INVALID, "psg_node_barrier_wait: null barrier");
+  const int gen = b->sh->generation.load(std::memory_order_acquire);
+  if (b->sh->count.fetch_add(1, std::memory_order_acq_rel) + 1 == b->nranks) {
+    b->sh->count.store(0, std::memory_order_relaxed);
+    b->sh->generation.fetch_add(1, std::memory_order_acq_rel);
+    return PSG_OK;
+  }
+  struct timespec t0, t;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (uint64_t spin = 0; b->sh->generation.load(std::memory_order_acquire) == gen; ++spin) {
+    if ((spin & 1023) == 1023) {
+      clock_gettime(CLOCK_MONOTONIC, &t);
+      const double el = (t.tv_sec - t0.tv_sec) + 1e-9 * (t.tv_nsec - t0.tv_nsec);
+      PSG_REQUIRE(el < timeout_s, PSG_ERR_COMM, "node barrier %s: timed out after %.1f s", b->name.c_str(), el);
+      if (el > 1e-3) usleep(20);
+    }
+  }
+  return PSG_OK;
+}
+
+int psg_node_barrier_destroy(psg_barrier* b) {
+  if (!b) return PSG_OK;
+  munmap(b->sh, 4096);
+  if (b->rank == 0) shm_unlink(b->name.c_str());
+  delete b;
+  return PSG_OK;
+}
+
+}  // extern "C"

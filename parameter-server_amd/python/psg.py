@@ -45,6 +45,9 @@ EXPORTS = [
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
     "psg_adam_create", "psg_adam_destroy", "psg_lr_apply",
+    "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
+    "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_node_barrier_create",
+    "psg_node_barrier_wait", "psg_node_barrier_destroy",
 ]
 
 
@@ -115,6 +118,13 @@ def lib() -> C.CDLL:
             "psg_adam_create": ([u64, f64, f64, f64, f64, C.POINTER(vp)], i32),
             "psg_adam_destroy": ([vp], i32),
             "psg_lr_apply": ([vp, vp, u64, f32, vp, i32, vp], i32),
+            "psg_ipc_handle_bytes": ([], i32), "psg_ipc_export": ([vp, vp], i32),
+            "psg_ipc_open": ([vp, C.POINTER(vp)], i32), "psg_ipc_close": ([vp], i32),
+            "psg_xgmi_create": ([i32, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)], i32),
+            "psg_xgmi_destroy": ([vp], i32), "psg_xgmi_push": ([vp, vp, u64, vp], i32),
+            "psg_xgmi_pull": ([vp, vp, vp, u64, vp], i32),
+            "psg_node_barrier_create": ([C.c_char_p, i32, i32, C.POINTER(vp)], i32),
+            "psg_node_barrier_wait": ([vp, f64], i32), "psg_node_barrier_destroy": ([vp], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -388,3 +398,56 @@ def lr_apply(weights: Store, merged, n: int, lr: float, adam: Adam | None, itera
              stream=None) -> None:
     _call("psg_lr_apply", weights.h, _ptr(merged), n, lr, adam.h if adam else None, iteration,
           _s(stream))
+
+
+# ---- one-shot xGMI exchange ----------------------------------------------------------
+def ipc_export(ptr) -> bytes:
+    n = lib().psg_ipc_handle_bytes()
+    buf = C.create_string_buffer(n)
+    _call("psg_ipc_export", C.c_void_p(_ptr(ptr)), buf)
+    return buf.raw
+
+
+def ipc_open(handle: bytes) -> int:
+    p = C.c_void_p(None)
+    _call("psg_ipc_open", C.create_string_buffer(handle, len(handle)), C.byref(p))
+    return p.value
+
+
+def ipc_close(ptr: int) -> None:
+    _call("psg_ipc_close", C.c_void_p(ptr))
+
+
+class Xgmi:
+    """psg_xgmi over peer pointers (own rank: local pointers; others: ipc_open'd)."""
+
+    def __init__(self, nranks: int, rank: int, vals_ptrs, store_ptrs):
+        self.h = C.c_void_p(None)
+        V = (C.c_void_p * nranks)(*vals_ptrs)
+        S = (C.c_void_p * nranks)(*store_ptrs)
+        _call("psg_xgmi_create", nranks, rank, V, S, C.byref(self.h))
+
+    def push(self, shard: Store, n_total: int, stream=None) -> None:
+        _call("psg_xgmi_push", self.h, shard.h, n_total, _s(stream))
+
+    def pull(self, shard: Store, out, n_total: int, stream=None) -> None:
+        _call("psg_xgmi_pull", self.h, shard.h, _ptr(out), n_total, _s(stream))
+
+    def close(self) -> None:
+        if self.h.value:
+            _call("psg_xgmi_destroy", self.h)
+            self.h = C.c_void_p(None)
+
+
+class NodeBarrier:
+    def __init__(self, name: str, nranks: int, rank: int):
+        self.h = C.c_void_p(None)
+        _call("psg_node_barrier_create", name.encode(), nranks, rank, C.byref(self.h))
+
+    def wait(self, timeout_s: float = 120.0) -> None:
+        _call("psg_node_barrier_wait", self.h, timeout_s)
+
+    def close(self) -> None:
+        if self.h.value:
+            _call("psg_node_barrier_destroy", self.h)
+            self.h = C.c_void_p(None)
