@@ -62,7 +62,11 @@ class GpuBackend:
         self.dt = {"f32": psg.F32, "f16": psg.F16}[dtype]
         self.vb = {"f32": 4, "f16": 2}[dtype]
         self.keyed = keyed
-        psg.set_device(local_rank)
+        # PSG_BENCH_SHARE_GPU=1 (testing only): ranks share the visible GPUs
+        # round-robin, and RCCL — which refuses two ranks on one GPU — is not
+        # used, so the xGMI exchange path of N > 1 can run on a 1-GPU box.
+        self.share_gpu = os.environ.get("PSG_BENCH_SHARE_GPU") == "1"
+        psg.set_device(local_rank % psg.device_count() if self.share_gpu else local_rank)
         self.stream = psg.Stream()
         self.comm = None
         self.xgmi = None
@@ -93,9 +97,10 @@ class GpuBackend:
         self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self._hi(), self.stream)
         self.out = p.DeviceBuffer(L * self.vb)
         if self.world > 1:
-            uid = [p.comm_id() if self.rank == 0 else None]
-            self.dist.broadcast_object_list(uid, src=0)
-            self.comm = p.Comm(uid[0], self.world, self.rank)
+            if not self.share_gpu:
+                uid = [p.comm_id() if self.rank == 0 else None]
+                self.dist.broadcast_object_list(uid, src=0)
+                self.comm = p.Comm(uid[0], self.world, self.rank)
             self.scratch = p.DeviceBuffer(blk * self.vb)
             if not self.keyed:
                 self._setup_xgmi()
@@ -186,10 +191,10 @@ class GpuBackend:
         (wall clock, barrier-synced): RCCL reduce-scatter then all-gather, the
         RCCL pipelined over 4/8/16 buckets, or the one-shot xGMI kernels.  The
         max over ranks decides, so every rank picks the same."""
-        if self.comm is None or self.keyed:
+        if self.world == 1 or self.keyed:
             return
         import torch
-        cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)]
+        cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
         if self.xgmi is not None:
             cands.append(("xgmi", 0))
         times = []
