@@ -1,0 +1,102 @@
+// svector_unit.cpp — SVector semantics the KV path relies on, following the
+// reference's own unit tests (src/utility/test/SVector_test.cpp): copy from a
+// std::vector, sharing copies, non-owning wraps, Slice aliasing and
+// detach-on-growth (SliceTest, :411-462), resize/fill, reinterpreting views,
+// FindRange.  Plain program (no PS node): exits non-zero on a failed CHECK.
+#include <cstdio>
+#include <memory>
+#include <vector>
+
+#include "ps/svector.h"
+
+using ps::SVector;
+
+int main() {
+  {  // construction from std::vector copies; copies of SVector share
+    std::vector<int> v{1, 2, 3};
+    SVector<int> s(v);
+    v[0] = 100;
+    CHECK_EQ(s[0], 1);
+    SVector<int> t = s;
+    t[1] = 20;
+    CHECK_EQ(s[1], 20);
+    CHECK_EQ(s.data(), t.data());
+  }
+  {  // shared_ptr<vector>: shares the vector's storage
+    auto sp = std::make_shared<std::vector<float>>(std::vector<float>{1.f, 2.f});
+    SVector<float> s(sp);
+    (*sp)[1] = 5.f;
+    CHECK_EQ(s[1], 5.f);
+  }
+  {  // raw pointer, non-owning
+    int raw[4] = {4, 3, 2, 1};
+    SVector<int> s(raw, 4);
+    raw[2] = 9;
+    CHECK_EQ(s[2], 9);
+    CHECK_EQ(s.size(), 4u);
+  }
+  {  // Slice aliases; growing the slice detaches it (SliceTest)
+    SVector<int> s1{1, 2, 3, 4, 5};
+    auto s2 = s1.Slice(2, 4);  // 3, 4
+    CHECK_EQ(s2[0], 3);
+    CHECK_EQ(s2[1], 4);
+    s1[2] = -3;
+    CHECK_EQ(s2[0], -3);
+    s2[1] = -4;
+    CHECK_EQ(s1[3], -4);
+    s2.push_back(999);  // capacity of a slice == its size: reallocates
+    CHECK_EQ(s2.size(), 3u);
+    CHECK_EQ(s2[1], -4);
+    CHECK_EQ(s2[2], 999);
+    s2[0] = 7;
+    CHECK_EQ(s1[2], -3);  // detached
+    CHECK_EQ(s1[4], 5);
+  }
+  {  // growing the parent detaches it from its slices
+    SVector<int> s1{1, 2, 3, 4};
+    SVector<int> s2 = s1.Slice(1, s1.size());
+    s2[1] = 30;
+    CHECK_EQ(s1[2], 30);
+    s1.push_back(5);
+    CHECK_EQ(s1.size(), 5u);
+    CHECK_EQ(s2.size(), 3u);
+    s1[2] = 99;
+    CHECK_EQ(s2[1], 30);
+  }
+  {  // resize fills new elements; shrink keeps the prefix
+    SVector<float> s;
+    s.resize(3, 1.5f);
+    CHECK_EQ(s.size(), 3u);
+    CHECK_EQ(s[2], 1.5f);
+    s.resize(5);
+    CHECK_EQ(s[4], 0.f);
+    s.resize(2);
+    CHECK_EQ(s.size(), 2u);
+    CHECK_EQ(s[1], 1.5f);
+  }
+  {  // reinterpreting views share the bytes (Message::AddData frames)
+    SVector<float> f{1.f, 2.f, 3.f};
+    SVector<char> c(f);
+    CHECK_EQ(c.size(), 12u);
+    SVector<float> back(c);
+    CHECK_EQ(back.size(), 3u);
+    CHECK_EQ(back[2], 3.f);
+    CHECK_EQ((void*)back.data(), (void*)f.data());
+    bool threw = false;
+    try {
+      SVector<char> odd(5);
+      SVector<float> bad(odd);  // 5 bytes are not whole floats
+    } catch (const ps_log::PSError&) {
+      threw = true;
+    }
+    CHECK(threw);
+  }
+  {  // FindRange (SVector.h:670-676)
+    SVector<uint64_t> k{2, 4, 6, 8};
+    ps::Range r = ps::FindRange<uint64_t>(k, 4, 8);
+    CHECK_EQ(r.begin, 1u);
+    CHECK_EQ(r.end, 3u);
+  }
+  std::printf("svector ok\n");
+  return 0;
+}

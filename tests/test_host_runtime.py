@@ -28,6 +28,15 @@ def _need(path):
         pytest.skip(f"{path} not built (make -C parameter-server_amd all)")
 
 
+def test_svector_semantics():
+    """SVector copy/share/Slice/detach/reinterpret semantics (SVector_test.cpp)."""
+    exe = os.path.join(BIN, "svector_unit")
+    _need(exe)
+    r = run(exe)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "svector ok" in r.stdout
+
+
 @pytest.mark.parametrize("ns,nw", [(1, 1), (2, 1), (3, 2), (8, 4)])
 def test_host_cluster(ns, nw):
     exe = os.path.join(BIN, "kv_cluster_host")
