@@ -245,11 +245,26 @@ class GpuBackend:
         a, b = self.new_event(), self.new_event()
         self.record(a)
         for _ in range(iters):
-            self.store.handle(self.p.PUSH, None, self.scratch, None, self.blk,
-                              first_key=self.rank * self.blk, stream=self.stream)
+            if self.mode == "xgmi":
+                # reads the peers' (constant) request vectors and writes only this
+                # rank's shard: safe to repeat without a barrier
+                self.xgmi.push(self.store, self.L, self.stream)
+            else:
+                self.store.handle(self.p.PUSH, None, self.scratch, None, self.blk,
+                                  first_key=self.rank * self.blk, stream=self.stream)
         self.record(b)
         self.sync()
         return self.elapsed(a, b) / iters
+
+    def probe_kernel(self):
+        """(name, algorithmic bytes per launch) of the kernel accumulate_probe times."""
+        if self.mode == "xgmi":
+            # store read + write (8 B) + one 4-B value from every rank's vector
+            return ("k_xgmi_push (fused reduce of %d ranks' blocks + accumulate; "
+                    "%d of them read over xGMI)" % (self.world, self.world - 1),
+                    (8 + self.vb * self.world) * self.blk)
+        return ("k_dense_vec<PUSH> on the shard after the reduce-scatter",
+                PUSH_ACCESSES * self.vb * self.blk)
 
     def check(self, steps_done: int) -> bool:
         """After `steps_done` pushes every shard holds steps * sum_w vals_w
@@ -386,6 +401,9 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
                                    "k_dense_vec<PUSH> (store += vals)", vb)
         res["pull_roofline_frac"] = round(PULL_ACCESSES * vb * blk / (pull_ms * 1e-3) / 1e9
                                           / HBM_PEAK_GBS, 4)
+    elif acc_ms is not None and hasattr(backend, "probe_kernel"):
+        kname, kbytes = backend.probe_kernel()
+        res["roofline"] = roofline(kbytes, acc_ms, args, kname, vb)
     elif acc_ms is not None:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, acc_ms, args,
                                    "k_dense_vec<PUSH> on the shard after the reduce-scatter", vb)
