@@ -109,27 +109,50 @@ class GpuBackend:
     def _setup_xgmi(self):
         """Map every peer's request vector and shard (hipIpc) for the one-shot
         xGMI exchange (psg_xgmi_push / _pull); a node barrier orders the phases."""
+        # Every step is agreed by all ranks (all_gather of a success flag), so a
+        # node where IPC mapping is unavailable falls back to RCCL everywhere
+        # instead of deadlocking.
         import uuid
         p = self.p
         self.xgmi = None
+        self._peer_ptrs = []
         sptr = self.store.info().vals
-        mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr))
+        try:
+            mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr))
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {self.rank}: hipIpc export unavailable ({e}); xGMI exchange off",
+                  file=sys.stderr)
+            mine = None
         allh = [None] * self.world
         self.dist.all_gather_object(allh, mine)
+        if any(h is None for h in allh):
+            return
         tag = [uuid.uuid4().hex[:16] if self.rank == 0 else None]
         self.dist.broadcast_object_list(tag, src=0)
-        self._peer_ptrs = []
-        vptrs, sptrs = [], []
-        for r in range(self.world):
-            if r == self.rank:
-                vptrs.append(self.vals.ptr)
-                sptrs.append(sptr)
-            else:
-                vptrs.append(p.ipc_open(allh[r][0]))
-                sptrs.append(p.ipc_open(allh[r][1]))
-                self._peer_ptrs += [vptrs[-1], sptrs[-1]]
-        self.xgmi = p.Xgmi(self.world, self.rank, vptrs, sptrs)
-        self.node_barrier = p.NodeBarrier("psg_bench_" + tag[0], self.world, self.rank)
+        vptrs, sptrs, ok = [], [], True
+        try:
+            for r in range(self.world):
+                if r == self.rank:
+                    vptrs.append(self.vals.ptr)
+                    sptrs.append(sptr)
+                else:
+                    vptrs.append(p.ipc_open(allh[r][0]))
+                    self._peer_ptrs.append(vptrs[-1])
+                    sptrs.append(p.ipc_open(allh[r][1]))
+                    self._peer_ptrs.append(sptrs[-1])
+            x = p.Xgmi(self.world, self.rank, vptrs, sptrs)
+            b = p.NodeBarrier("psg_bench_" + tag[0], self.world, self.rank)
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {self.rank}: xGMI mapping failed ({e}); xGMI exchange off", file=sys.stderr)
+            ok = False
+        oks = [None] * self.world
+        self.dist.all_gather_object(oks, ok)
+        if not all(oks):
+            for ptr in self._peer_ptrs:
+                p.ipc_close(ptr)
+            self._peer_ptrs = []
+            return
+        self.xgmi, self.node_barrier = x, b
         self.node_barrier.wait()
 
     def _key_pos(self):
