@@ -149,9 +149,23 @@ static DenseCfg dense_cfg() {
   }();
   return cfg;
 }
-static DenseCfg dense_cfg_for(uint64_t store_bytes) {
+static DenseCfg dense_cfg_for(uint64_t store_bytes, int op) {
   DenseCfg c = dense_cfg();
-  if (c.nt < 0) c.nt = store_bytes > (512ull << 20) ? 3 : 1;
+  if (c.nt >= 0) return c;  // explicit sweep settings
+  if (store_bytes <= (512ull << 20)) {
+    c.nt = 1;
+  } else {
+    // past the Infinity Cache (profiles/r1_sweep_dense_256M.json): Push 1 vector
+    // per lane at 2 blocks/CU, Pull 2 vectors at 4 blocks/CU, all non-temporal
+    c.nt = 3;
+    if (op == PSG_PULL) {
+      c.unroll = 2;
+      c.blocks_per_cu = 4;
+    } else {
+      c.unroll = 1;
+      c.blocks_per_cu = 2;
+    }
+  }
   return c;
 }
 
@@ -192,7 +206,7 @@ static int run_dense(void* store, const void* vals, void* out, uint64_t n, hipSt
   const bool need_vals = (OP & PSG_PUSH) != 0, need_out = (OP & PSG_PULL) != 0;
   bool vec_ok = aligned16(store) && (!need_vals || aligned16(vals)) && (!need_out || aligned16(out));
   uint64_t nvec = vec_ok ? n / kVec : 0;
-  if (nvec) dispatch_vec<DT, OP>(dense_cfg_for(n * sizeof(T)), store, vals, out, nvec, s);
+  if (nvec) dispatch_vec<DT, OP>(dense_cfg_for(n * sizeof(T), OP), store, vals, out, nvec, s);
   uint64_t done = nvec * kVec;
   if (done < n) {
     uint64_t rest = n - done;
