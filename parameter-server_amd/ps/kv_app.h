@@ -66,7 +66,7 @@ int DeviceOf(const SVector<T>* v) { return v->device(); }
 template <typename T>
 SVector<T> ToHost(const SVector<T>& v) {
   if (!v.on_device() || v.empty()) return v;
-  SVector<T> h(v.size());
+  SVector<T> h = SVector<T>::Uninitialized(v.size());
   device::CopySync(h.data(), v.data(), v.size() * sizeof(T), 1);
   return h;
 }
@@ -575,7 +575,7 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
   if (ndev == 0 && out_dev < 0) {
     Value* p = vals->data();
     for (const auto& r : kvs) {
-      if (r.kv.vals.size()) std::memcpy(p, r.kv.vals.data(), r.kv.vals.size() * sizeof(Value));
+      if (r.kv.vals.size()) HostCopy(p, r.kv.vals.data(), r.kv.vals.size() * sizeof(Value));
       p += r.kv.vals.size();
     }
   } else if (total_val) {

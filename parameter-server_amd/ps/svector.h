@@ -34,6 +34,11 @@ std::shared_ptr<void> Alloc(size_t bytes, int device);
 std::shared_ptr<void> HostAlloc(size_t bytes);
 }  // namespace device
 
+/* memcpy that splits copies of >= 16 MiB over several host threads (the
+ * vector -> SVector copy of KVWorker::Push, the pull merge into the caller's
+ * vector); implemented in src/device.cc. */
+void HostCopy(void* dst, const void* src, size_t bytes);
+
 template <typename T>
 class SVector {
   static_assert(std::is_trivially_copyable<T>::value, "SVector holds trivially copyable types");
@@ -87,6 +92,14 @@ class SVector {
     return *this;
   }
 
+  /* `count` host elements left uninitialised (a buffer a copy will fill) */
+  static SVector Uninitialized(size_t count) {
+    SVector v;
+    v.reserve(count);
+    v.size_ = count;
+    return v;
+  }
+
   /* ---- HBM arrays ---- */
   /* `count` uninitialised elements in the pool of GPU `device` */
   static SVector OnDevice(size_t count, int device) {
@@ -128,8 +141,9 @@ class SVector {
   void CopyFrom(const T* src, size_t n) {
     CHECK(!on_device()) << "CopyFrom into a device SVector";
     clear();
-    resize(n);
-    if (n) std::memcpy(data(), src, n * sizeof(T));
+    reserve(n);
+    size_ = n;
+    if (n) HostCopy(data(), src, n * sizeof(T));
   }
   template <typename It>
   void CopyFrom(It first, It last) {

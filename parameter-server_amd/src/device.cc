@@ -1,8 +1,12 @@
 // device.cc — GPU plumbing of the host runtime, all through the psg C-ABI.
 #include "internal/device.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ps/log.h"
@@ -168,4 +172,30 @@ void Merge(std::vector<psg_segment>* segs, int elem_size, void* dst, uint64_t ds
 }
 
 }  // namespace device
+
+void HostCopy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kSplit = size_t(16) << 20;
+  static const int nthreads = [] {
+    unsigned hc = std::thread::hardware_concurrency();
+    const char* e = std::getenv("PS_COPY_THREADS");
+    int n = e ? std::atoi(e) : (int)std::min<unsigned>(hc ? hc / 2 : 4, 8u);
+    return std::max(1, n);
+  }();
+  if (bytes < kSplit || nthreads == 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const int parts = (int)std::min<size_t>((size_t)nthreads, bytes / (kSplit / 4));
+  const size_t chunk = (bytes / parts + 4095) & ~size_t(4095);
+  std::vector<std::thread> ts;
+  for (int i = 1; i < parts; ++i) {
+    const size_t off = chunk * i;
+    if (off >= bytes) break;
+    const size_t len = std::min(chunk, bytes - off);
+    ts.emplace_back([=] { std::memcpy((char*)dst + off, (const char*)src + off, len); });
+  }
+  std::memcpy(dst, src, std::min(chunk, bytes));
+  for (auto& t : ts) t.join();
+}
+
 }  // namespace ps
