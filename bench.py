@@ -234,11 +234,38 @@ class GpuBackend:
             dist.barrier()
         t = torch.tensor(times, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        best = int(t.argmin().item())
-        self._set_mode(cands[best])
+        order = sorted(range(len(cands)), key=lambda i: t[i].item())
+        self._set_mode(cands[order[0]])
         self.calibration = {f"{m}{'' if m == 'xgmi' else '/' + str(nb)}": round(x, 4)
                             for (m, nb), x in zip(cands, t.tolist())}
         self.pushes_in_calibration = len(cands) * (iters + 1)
+        if self.mode == "xgmi":
+            self.pushes_in_calibration += 1
+            self.exchange_verified = self._verify_xgmi(dist)
+            if not self.exchange_verified:
+                rest = [cands[i] for i in order if cands[i][0] != "xgmi"]
+                if not rest:
+                    raise RuntimeError("xGMI exchange failed its checksum verification "
+                                       "and no RCCL communicator is available")
+                print("xGMI exchange failed its checksum verification; using RCCL",
+                      file=sys.stderr)
+                self._set_mode(rest[0])
+
+    def _verify_xgmi(self, dist) -> bool:
+        """One xGMI Push + Pull, then every rank's pulled block w must carry the
+        same psg_checksum as rank w's own shard (read locally): catches a stale
+        or torn cross-GPU read before the timed steps rely on the path."""
+        p = self.p
+        self.push()
+        self.pull()
+        nb = self.blk * self.vb
+        mine = p.checksum(self.store.info().vals, nb, self.stream)
+        got = [p.checksum(self.out.ptr + w * nb, nb, self.stream) for w in range(self.world)]
+        owners = [None] * self.world
+        dist.all_gather_object(owners, mine)
+        ok = [None] * self.world
+        dist.all_gather_object(ok, got == owners)
+        return all(ok)
 
     def _one_step(self):
         if self.fused:
@@ -415,6 +442,8 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
             res["config"]["exchange"] = ("RCCL pipelined reduce/broadcast, %d buckets" % backend.nbuckets
                                          if fused else "RCCL reduce-scatter then all-gather")
         res["config"]["calibration_ms"] = getattr(backend, "calibration", None)
+        if hasattr(backend, "exchange_verified"):
+            res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
     if world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
                                    "SORTED-store Push: psg_slice + k_tile_windows + k_resolve + "

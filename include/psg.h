@@ -128,6 +128,12 @@ int psg_fill_synth(void* dptr, uint64_t n, int dtype, uint64_t seed, int mode,
  * `kMaxKey / num * i + rank`, tests/test_kv_app_benchmark.cpp:47-52). */
 int psg_fill_keys_arith(uint64_t* keys, uint64_t n, uint64_t base, uint64_t step,
                         psg_stream stream);
+/* Position-keyed checksum of a device range (nbytes % 8 == 0, 8-B aligned):
+ * sum over 64-bit words i of splitmix64(w_i ^ i * 0x9e3779b97f4a7c15), mod
+ * 2^64.  Synchronises `stream`.  Used to verify an exchange end to end (the
+ * xGMI pull against the owners' shards) without moving the data to the host.
+ * No reference counterpart: test/verification support. */
+int psg_checksum(const void* dptr, uint64_t nbytes, uint64_t* sum_host, psg_stream stream);
 
 /* ======================================================================== */
 /* Server-side value store  (KVServerDefaultHandle::store, KVApp.h:457)      */

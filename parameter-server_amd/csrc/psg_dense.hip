@@ -149,17 +149,46 @@ static DenseCfg dense_cfg() {
   }();
   return cfg;
 }
+// PSG_DENSE_PULL_{UNROLL,NT,BPC}: the same knobs for the Pull alone (sweeps).
+static DenseCfg dense_pull_override() {
+  static DenseCfg cfg = [] {
+    DenseCfg c;
+    c.unroll = c.blocks_per_cu = 0;
+    c.nt = -1;
+    if (const char* e = getenv("PSG_DENSE_PULL_UNROLL")) c.unroll = atoi(e);
+    if (const char* e = getenv("PSG_DENSE_PULL_NT")) c.nt = atoi(e);
+    if (const char* e = getenv("PSG_DENSE_PULL_BPC")) c.blocks_per_cu = atoi(e);
+    if (c.unroll != 1 && c.unroll != 2 && c.unroll != 4 && c.unroll != 8) c.unroll = 0;
+    if (c.blocks_per_cu < 1 || c.blocks_per_cu > 32) c.blocks_per_cu = 0;
+    if (c.nt < -1 || c.nt > 3) c.nt = -1;
+    return c;
+  }();
+  return cfg;
+}
+static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op);
 static DenseCfg dense_cfg_for(uint64_t store_bytes, int op) {
+  DenseCfg c = dense_cfg_for_size(store_bytes, op);
+  if (op == PSG_PULL) {
+    const DenseCfg& o = dense_pull_override();
+    if (o.unroll) c.unroll = o.unroll;
+    if (o.nt >= 0) c.nt = o.nt;
+    if (o.blocks_per_cu) c.blocks_per_cu = o.blocks_per_cu;
+  }
+  return c;
+}
+static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op) {
   DenseCfg c = dense_cfg();
   if (c.nt >= 0) return c;  // explicit sweep settings
   if (store_bytes <= (512ull << 20)) {
     c.nt = 1;
   } else {
-    // past the Infinity Cache (profiles/r1_sweep_dense_256M.json): Push 1 vector
-    // per lane at 2 blocks/CU, Pull 2 vectors at 4 blocks/CU, all non-temporal
+    // past the Infinity Cache (profiles/r1_sweep_dense_256M.json and the
+    // Pull-only sweep profiles/r1_sweep_pull_256M.json): 1 vector per lane,
+    // all non-temporal; Push at 2 blocks/CU, Pull at 4 (0.80 of 8 TB/s, up
+    // from 0.72 with 2 vectors per lane)
     c.nt = 3;
     if (op == PSG_PULL) {
-      c.unroll = 2;
+      c.unroll = 1;
       c.blocks_per_cu = 4;
     } else {
       c.unroll = 1;

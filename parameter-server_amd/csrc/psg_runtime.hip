@@ -2,6 +2,7 @@
 // memory, streams, events, seeded synthetic data.
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "psg_internal.h"
 
@@ -66,6 +67,28 @@ __global__ __launch_bounds__(256) void k_keys_arith(uint64_t* __restrict__ keys,
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x)
     keys[i] = base + i * step;
+}
+
+// Position-keyed checksum of n 64-bit words: sum_i splitmix64(w_i ^ (i * phi))
+// (mod 2^64).  One wave-reduced partial per block; the host adds the partials.
+__global__ __launch_bounds__(256) void k_checksum(const uint64_t* __restrict__ w, uint64_t n,
+                                                  uint64_t* __restrict__ partials) {
+  uint64_t h = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    h += splitmix64(__builtin_nontemporal_load(w + i) ^ (i * 0x9e3779b97f4a7c15ull));
+  for (int o = 32; o > 0; o >>= 1) {  // 64-bit butterfly as two 32-bit shuffles
+    const uint32_t lo = __shfl_xor((uint32_t)h, o, 64), hi = __shfl_xor((uint32_t)(h >> 32), o, 64);
+    h += ((uint64_t)hi << 32) | lo;
+  }
+  __shared__ uint64_t part[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int k = 0; k < kBlock / 64; ++k) t += part[k];
+    partials[blockIdx.x] = t;
+  }
 }
 
 static unsigned grid_for(uint64_t n) {
@@ -235,6 +258,32 @@ int psg_fill_keys_arith(uint64_t* keys, uint64_t n, uint64_t base, uint64_t step
   PSG_REQUIRE(keys, PSG_ERR_INVALID, "psg_fill_keys_arith: null pointer");
   k_keys_arith<<<grid_for(n), kBlock, 0, (hipStream_t)stream>>>(keys, n, base, step);
   PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int psg_checksum(const void* dptr, uint64_t nbytes, uint64_t* sum_host, psg_stream stream) {
+  PSG_REQUIRE(sum_host, PSG_ERR_INVALID, "psg_checksum: null out");
+  PSG_REQUIRE(nbytes % 8 == 0 && ((uintptr_t)dptr & 7u) == 0, PSG_ERR_INVALID,
+              "psg_checksum: need 8-B aligned pointer and a multiple of 8 bytes");
+  *sum_host = 0;
+  if (nbytes == 0) return PSG_OK;
+  PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_checksum: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t n = nbytes / 8;
+  const unsigned g = grid_for(n);
+  uint64_t* part = nullptr;
+  PSG_HIP(hipMalloc((void**)&part, (size_t)g * sizeof(uint64_t)));
+  std::vector<uint64_t> host(g);
+  k_checksum<<<g, kBlock, 0, s>>>((const uint64_t*)dptr, n, part);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(host.data(), part, (size_t)g * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(part);
+  if (e != hipSuccess) return hip_fail(e, "psg_checksum", __FILE__, __LINE__);
+  uint64_t h = 0;
+  for (uint64_t x : host) h += x;
+  *sum_host = h;
   return PSG_OK;
 }
 

@@ -38,7 +38,7 @@ EXPORTS = [
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
     "psg_memset", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
     "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
-    "psg_event_elapsed_ms", "psg_fill_synth", "psg_fill_keys_arith",
+    "psg_event_elapsed_ms", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
     "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
@@ -95,6 +95,7 @@ def lib() -> C.CDLL:
             "psg_event_elapsed_ms": ([vp, vp, C.POINTER(f32)], i32),
             "psg_fill_synth": ([vp, u64, i32, u64, i32, f64, f64, vp], i32),
             "psg_fill_keys_arith": ([vp, u64, u64, u64, vp], i32),
+            "psg_checksum": ([vp, u64, C.POINTER(u64), vp], i32),
             "psg_store_create": ([i32, i32, u64, u64, u64, C.POINTER(vp)], i32),
             "psg_store_destroy": ([vp], i32),
             "psg_store_get_info": ([vp, C.POINTER(StoreInfo)], i32),
@@ -260,6 +261,25 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def checksum(ptr, nbytes: int, stream=None) -> int:
+    """psg_checksum of a device range (synchronises the stream)."""
+    h = C.c_uint64(0)
+    _call("psg_checksum", C.c_void_p(_ptr(ptr)), C.c_uint64(nbytes), C.byref(h), _s(stream))
+    return h.value
+
+
+def checksum_host(a: np.ndarray) -> int:
+    """The same checksum computed with numpy (for tests)."""
+    w = np.ascontiguousarray(a).view(np.uint64)
+    with np.errstate(over="ignore"):
+        x = w ^ (np.arange(len(w), dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+        return int(x.sum(dtype=np.uint64))
 
 
 # ---- value store ----------------------------------------------------------------

@@ -396,3 +396,21 @@ def test_comm_single_rank_push_pull(force, dtype, n, monkeypatch):
         exp = orc.handle(oracle.PUSH | oracle.PULL, None, hv, n)
         np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"nbuckets={nb}")
     c.close()
+
+
+@pytest.mark.parametrize("nbytes", [0, 8, 4096, 8 * 1000003])
+def test_checksum_matches_host(nbytes):
+    """psg_checksum (the exchange self-check bench.py runs after choosing the
+    xGMI path) equals its numpy restatement, and moves with one changed word."""
+    a = np.random.default_rng(5).integers(0, 1 << 63, nbytes // 8, dtype=np.uint64)
+    b = psg.DeviceBuffer(max(nbytes, 8))
+    b.upload(a)
+    assert psg.checksum(b, nbytes) == psg.checksum_host(a)
+    if nbytes >= 16:
+        a[1] ^= np.uint64(1)
+        b.upload(a)
+        assert psg.checksum(b, nbytes) == psg.checksum_host(a)
+        # swapped words change it (position-keyed)
+        a[[0, 1]] = a[[1, 0]]
+        b.upload(a)
+        assert psg.checksum(b, nbytes) == psg.checksum_host(a)

@@ -116,3 +116,28 @@ def test_xgmi_exchange_multiprocess(world):
         p.join(60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert all(ok for _, _, ok in results), results
+
+
+@pytest.mark.gpu
+def test_bench_n2_shared_gpu_xgmi_verified():
+    """bench.py's N>1 path end to end with two ranks on one GPU
+    (PSG_BENCH_SHARE_GPU=1: the xGMI exchange, no RCCL): the calibration's
+    checksum verification of the pulled shards must pass and the closed-form
+    parity check must hold after every push the run made."""
+    import json
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PSG_BENCH_SHARE_GPU="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--keys", str(1 << 22),
+           "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["parity_check"] is True, res
+    assert res["config"].get("xgmi_checksum_verified") is True, res
