@@ -276,6 +276,10 @@ typedef struct psg_xgmi psg_xgmi;
 typedef struct psg_barrier psg_barrier;
 int psg_ipc_handle_bytes(void);
 int psg_ipc_export(const void* dptr, void* handle_out);   /* dptr: start of an allocation */
+/* the same for a pointer anywhere inside an allocation: the handle of the
+ * allocation and dptr's byte offset in it (the process-mode Van ships HBM
+ * frames — slices of pooled blocks — this way: parameter-server_amd/src/tcp_van.cc) */
+int psg_ipc_export_range(const void* dptr, void* handle_out, uint64_t* offset_out);
 int psg_ipc_open(const void* handle, void** dptr_out);
 int psg_ipc_close(void* dptr);
 /* peer_vals[r] / peer_stores[r]: rank r's request vector (n_total values) and

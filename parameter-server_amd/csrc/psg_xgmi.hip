@@ -100,6 +100,18 @@ int psg_ipc_export(const void* dptr, void* handle_out) {
   return PSG_OK;
 }
 
+int psg_ipc_export_range(const void* dptr, void* handle_out, uint64_t* offset_out) {
+  PSG_REQUIRE(dptr && handle_out && offset_out, PSG_ERR_INVALID, "psg_ipc_export_range: null argument");
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  PSG_HIP(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)const_cast<void*>(dptr)));
+  hipIpcMemHandle_t h;
+  PSG_HIP(hipIpcGetMemHandle(&h, (void*)base));
+  memcpy(handle_out, &h, sizeof(h));
+  *offset_out = (uint64_t)((const char*)dptr - (const char*)base);
+  return PSG_OK;
+}
+
 int psg_ipc_open(const void* handle, void** dptr_out) {
   PSG_REQUIRE(handle && dptr_out, PSG_ERR_INVALID, "psg_ipc_open: null argument");
   hipIpcMemHandle_t h;

@@ -31,7 +31,9 @@ class PostOffice {
   static PostOffice* Get();
   static PostOffice* GetIfBound();
 
-  PostOffice(Node::Role role, int rank, int num_servers, int num_workers, int device);
+  /* van_type: PS_VAN_TYPE when null ("local" by default) */
+  PostOffice(Node::Role role, int rank, int num_servers, int num_workers, int device,
+             const char* van_type = nullptr);
   ~PostOffice();
 
   void Start(int customer_id, const char* config_filename, const char* log_filename,
@@ -72,6 +74,8 @@ class PostOffice {
   std::vector<int> GetDeadNodes(int t = 60) { (void)t; return {}; }
   /* set the calling thread's node (and its GPU) */
   void BindThread();
+  /* process mode: the rank the scheduler assigned and the GPU it implies */
+  void SetIdentity(int rank, int device);
 
  private:
   Node::Role role_;
@@ -110,11 +114,32 @@ PostOffice* NodeByArgv(char** argv);
 void Barrier(PostOffice* po, int customer_id, int group);
 void NoteStarted(PostOffice* po, int customer_id);
 void Deliver(const Message& msg);
+/* hand msg to the right customer of node dst (Van.cpp:226-237) */
+void DeliverTo(PostOffice* dst, const Message& msg);
 /* wake every waiter with an error after a node failed */
 void Abort(const std::string& why);
 bool Aborted();
 std::string AbortReason();
 bool Configured();
 }  // namespace cluster
+
+/* Process mode: one node per OS process, as tests/local.py launches the
+ * reference (local.py:87-114: argv = {prog, config.json, log, role}).  Nodes
+ * find each other through the scheduler (PS_SCHEDULER_URI / _PORT) over TCP;
+ * host frames travel on the socket, HBM frames as hipIpc handles that the
+ * receiver maps in place (src/tcp_van.cc). */
+namespace proc {
+/* this process runs one node (RunNode) */
+bool Active();
+PostOffice* Node();
+/* the role named by argv[3] or PS_ROLE ("scheduler" / "server" / "worker"), or
+ * nullptr when this is not a process-mode launch */
+const char* RoleOf(int argc, char** argv);
+/* run node_main as the one node of this process */
+int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** argv);
+/* local.py's job in C++: start one scheduler, num_servers servers and
+ * num_workers workers of this executable as separate processes and wait */
+int Launch(int num_servers, int num_workers, int argc, char** argv);
+}  // namespace proc
 
 }  // namespace ps

@@ -39,6 +39,7 @@ struct Node {
   std::string hostname = "local";
   int port = 0;
   bool is_recovered = false;
+  bool gpu = false;  // process mode: the node can map HBM frames (it sees a GPU)
   std::string DebugString() const {
     std::ostringstream os;
     os << (role == SERVER ? "server" : role == WORKER ? "worker" : "scheduler") << "[" << id << "]";
@@ -47,7 +48,10 @@ struct Node {
 };
 
 struct Control {
-  enum Command { EMPTY, TERMINATE, ADD_NODE, BARRIER, ACK, HEARTBEAT };
+  // STARTED / RELEASE_FRAME / ABORT are this runtime's own (process mode,
+  // src/tcp_van.cc): a customer started; an HBM frame a peer mapped is no
+  // longer referenced; the job failed.
+  enum Command { EMPTY, TERMINATE, ADD_NODE, BARRIER, ACK, HEARTBEAT, STARTED, RELEASE_FRAME, ABORT };
   Command cmd = EMPTY;
   std::vector<Node> nodes;
   int barrier_group = 0;

@@ -30,6 +30,20 @@ class Van {
   const Node& my_node() const { return my_node_; }
   bool IsReady() const { return ready_.load(); }
   int GetAvailableTimestamp() { return timestamp_++; }
+
+  /* Process mode (one node per process, src/tcp_van.cc): the barrier runs
+   * through the scheduler (Van.cpp:186-216) and returns true; the local Van
+   * returns false and the in-process cluster barrier is used. */
+  virtual bool Barrier(int customer_id, int group) {
+    (void)customer_id;
+    (void)group;
+    return false;
+  }
+  /* a customer of this node called Start (the scheduler counts customer-c
+   * barriers over the nodes where customer c exists) */
+  virtual void NoteStarted(int customer_id) { (void)customer_id; }
+  /* tell the other processes the job failed (their waiters then throw) */
+  virtual void NotifyAbort(const std::string& why) { (void)why; }
   uint64_t send_bytes() const { return send_bytes_.load(); }
   uint64_t receive_bytes() const { return receive_bytes_.load(); }
   void CountReceived(uint64_t b) { receive_bytes_ += b; }
@@ -48,5 +62,8 @@ class Van {
 
   friend class PostOffice;
 };
+
+/* the process-mode Van (src/tcp_van.cc) */
+Van* NewTcpVan(PostOffice* po);
 
 }  // namespace ps

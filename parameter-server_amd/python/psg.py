@@ -45,7 +45,7 @@ EXPORTS = [
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
     "psg_adam_create", "psg_adam_destroy", "psg_lr_apply",
-    "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
+    "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
     "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_node_barrier_create",
     "psg_node_barrier_wait", "psg_node_barrier_destroy",
 ]
@@ -120,6 +120,7 @@ def lib() -> C.CDLL:
             "psg_adam_destroy": ([vp], i32),
             "psg_lr_apply": ([vp, vp, u64, f32, vp, i32, vp], i32),
             "psg_ipc_handle_bytes": ([], i32), "psg_ipc_export": ([vp, vp], i32),
+            "psg_ipc_export_range": ([vp, vp, C.POINTER(u64)], i32),
             "psg_ipc_open": ([vp, C.POINTER(vp)], i32), "psg_ipc_close": ([vp], i32),
             "psg_xgmi_create": ([i32, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)], i32),
             "psg_xgmi_destroy": ([vp], i32), "psg_xgmi_push": ([vp, vp, u64, vp], i32),

@@ -74,11 +74,15 @@ void Abort(const std::string& why) {
   }
   s.cv.notify_all();
   LOG(ERROR) << "job aborted: " << why;
+  if (proc::Active()) proc::Node()->van()->NotifyAbort(why);
 }
 
 void NoteStarted(PostOffice* po, int customer_id) {
-  std::lock_guard<std::mutex> lk(S().mu);
-  S().started[po->my_id()].insert(customer_id);
+  {
+    std::lock_guard<std::mutex> lk(S().mu);
+    S().started[po->my_id()].insert(customer_id);
+  }
+  po->van()->NoteStarted(customer_id);
 }
 
 // Barrier per (group, customer_id): customer 0 of every node in the group
@@ -88,6 +92,7 @@ void NoteStarted(PostOffice* po, int customer_id) {
 void Barrier(PostOffice* po, int customer_id, int group) {
   const auto& ids = po->GetNodeIDs(group);
   if (ids.size() <= 1) return;
+  if (po->van()->Barrier(customer_id, group)) return;  // process mode: via the scheduler
   ClusterState& s = S();
   std::unique_lock<std::mutex> lk(s.mu);
   int participants = (int)ids.size();
@@ -117,6 +122,10 @@ void Barrier(PostOffice* po, int customer_id, int group) {
 void Deliver(const Message& msg) {
   PostOffice* dst = NodeById(msg.meta.receiver);
   CHECK(dst) << "no node with id " << msg.meta.receiver;
+  DeliverTo(dst, msg);
+}
+
+void DeliverTo(PostOffice* dst, const Message& msg) {
   // only workers run several customers per app (Van.cpp:246-257)
   const int cid = dst->is_worker() ? msg.meta.customer_id : msg.meta.app_id;
   Customer* c = dst->GetCustomer(msg.meta.app_id, cid, 5);
@@ -129,18 +138,23 @@ void Deliver(const Message& msg) {
 }  // namespace cluster
 
 // ---------------------------------------------------------------------------
-PostOffice* PostOffice::GetIfBound() { return t_node; }
+PostOffice* PostOffice::GetIfBound() { return t_node ? t_node : (proc::Active() ? proc::Node() : nullptr); }
 
 PostOffice* PostOffice::Get() {
+  if (!t_node && proc::Active()) return proc::Node();  // one node per process
   if (!t_node)
     LOG(FATAL) << "this thread belongs to no PS node: run the program under a ps launcher "
                   "(ps::RunLocalCluster / ps_launch)";
   return t_node;
 }
 
-PostOffice::PostOffice(Node::Role role, int rank, int num_servers, int num_workers, int device)
+PostOffice::PostOffice(Node::Role role, int rank, int num_servers, int num_workers, int device,
+                       const char* van_type)
     : role_(role), rank_(rank), num_servers_(num_servers), num_workers_(num_workers), device_(device) {
-  id_ = role == Node::SCHEDULER ? kScheduler : role == Node::SERVER ? ServerRankToID(rank) : WorkerRankToID(rank);
+  id_ = role == Node::SCHEDULER ? kScheduler
+        : rank < 0              ? Node::kEmpty  // process mode: assigned by the scheduler
+        : role == Node::SERVER  ? ServerRankToID(rank)
+                                : WorkerRankToID(rank);
   // group -> node ids (PostOffice.cpp:50-73)
   for (int i = 0; i < num_servers_; ++i) {
     int id = ServerRankToID(i);
@@ -157,8 +171,14 @@ PostOffice::PostOffice(Node::Role role, int rank, int num_servers, int num_worke
   for (int g : {kScheduler, kScheduler + kServerGroup, kScheduler + kWorkerGroup,
                 kScheduler + kServerGroup + kWorkerGroup})
     node_ids_[g].push_back(kScheduler);
-  const char* vt = std::getenv("PS_VAN_TYPE");
+  const char* vt = van_type ? van_type : std::getenv("PS_VAN_TYPE");
   van_.reset(Van::Create(vt ? vt : "local", this));
+}
+
+void PostOffice::SetIdentity(int rank, int device) {
+  rank_ = rank;
+  id_ = role_ == Node::SCHEDULER ? kScheduler : role_ == Node::SERVER ? ServerRankToID(rank) : WorkerRankToID(rank);
+  device_ = device;
 }
 
 PostOffice::~PostOffice() {
@@ -188,7 +208,7 @@ void PostOffice::Start(int customer_id, const char* config_filename, const char*
       start_stage_ = 1;
     }
   }
-  if (t_node != this) BindThread();
+  BindThread();  // process mode: the GPU is known only after registration
   cluster::NoteStarted(this, customer_id);
   if (need_barrier) Barrier(customer_id, kAllNodes);
 }

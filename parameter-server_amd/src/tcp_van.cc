@@ -1,0 +1,1026 @@
+// tcp_van.cc — process mode: one node per OS process, the way tests/local.py
+// runs the reference (local.py:87-114: argv = {prog, config.json, log, role}),
+// a TCP Van between the processes, and a launcher that does local.py's job.
+//
+// Control plane (the reference's Van.cpp:181-442, re-designed for one host):
+//   * every server / worker binds a listening socket and sends ADD_NODE to the
+//     scheduler at PS_SCHEDULER_URI:PS_SCHEDULER_PORT;
+//   * once PS_NUM_SERVER + PS_NUM_WORKER nodes registered, the scheduler orders
+//     them as Van.cpp:292-296 does (hostname descending, port ascending), gives
+//     server / worker ranks in that order and sends every node the table;
+//   * BARRIER requests go to the scheduler, which releases a group once all its
+//     members arrived (for customer c > 0: the members on which customer c
+//     started — the in-process rule of cluster::Barrier);
+//   * a failed CHECK anywhere is broadcast (ABORT), and a peer that disconnects
+//     without TERMINATE aborts the job, so no process waits forever.
+// Data plane:
+//   * host frames are written to the socket (the ZMQ frames of
+//     ZMQVan.cpp:147-248);
+//   * HBM frames are not copied: the sender ships the hipIpc handle and offset
+//     of the frame (psg_ipc_export_range) and keeps the frame alive; the
+//     receiver maps the allocation once (psg_ipc_open, cached) and wraps the
+//     bytes as an HBM SVector whose last reference sends RELEASE_FRAME back.
+//     The server's kernel then reads a worker's keys / values in place — over
+//     xGMI when the worker runs on another GPU.  Frames for a node without a
+//     GPU or on another host are staged through host memory.
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <set>
+#include <thread>
+#include <unordered_map>
+
+#include "internal/Env.h"
+#include "internal/PostOffice.h"
+#include "internal/device.h"
+
+extern char** environ;
+
+namespace ps {
+
+namespace {
+
+constexpr uint32_t kMagic = 0x31475350;  // "PSG1"
+constexpr int kHandleBytes = 64;         // sizeof(hipIpcMemHandle_t)
+
+// ---- socket helpers -----------------------------------------------------------
+bool WriteAll(int fd, const void* buf, size_t n) {
+  const char* p = static_cast<const char*>(buf);
+  while (n) {
+    ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+bool ReadAll(int fd, void* buf, size_t n) {
+  char* p = static_cast<char*>(buf);
+  while (n) {
+    ssize_t r = ::recv(fd, p, n, 0);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    p += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+void Tune(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int buf = 8 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
+}
+
+bool Resolve(const std::string& host, int port, sockaddr_in* sa) {
+  std::memset(sa, 0, sizeof(*sa));
+  sa->sin_family = AF_INET;
+  sa->sin_port = htons((uint16_t)port);
+  if (inet_pton(AF_INET, host.c_str(), &sa->sin_addr) == 1) return true;
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  if (getaddrinfo(host.c_str(), nullptr, &hints, &res) != 0 || !res) return false;
+  sa->sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+  freeaddrinfo(res);
+  return true;
+}
+
+// ---- message codec ------------------------------------------------------------
+struct Writer {
+  std::string b;
+  template <typename T>
+  void pod(const T& v) {
+    b.append(reinterpret_cast<const char*>(&v), sizeof(T));
+  }
+  void str(const std::string& s) {
+    pod<uint32_t>((uint32_t)s.size());
+    b.append(s);
+  }
+};
+
+struct Reader {
+  const char* p;
+  const char* e;
+  template <typename T>
+  T pod() {
+    CHECK(p + sizeof(T) <= e) << "truncated message";
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+  }
+  std::string str() {
+    const uint32_t n = pod<uint32_t>();
+    CHECK(p + n <= e) << "truncated message";
+    std::string s(p, n);
+    p += n;
+    return s;
+  }
+};
+
+void PutNode(Writer& w, const Node& n) {
+  w.pod<int32_t>(n.role);
+  w.pod<int32_t>(n.id);
+  w.pod<int32_t>(n.customer_id);
+  w.str(n.hostname);
+  w.pod<int32_t>(n.port);
+  w.pod<uint8_t>(n.is_recovered);
+  w.pod<uint8_t>(n.gpu);
+}
+
+Node GetNode(Reader& r) {
+  Node n;
+  n.role = (Node::Role)r.pod<int32_t>();
+  n.id = r.pod<int32_t>();
+  n.customer_id = r.pod<int32_t>();
+  n.hostname = r.str();
+  n.port = r.pod<int32_t>();
+  n.is_recovered = r.pod<uint8_t>() != 0;
+  n.gpu = r.pod<uint8_t>() != 0;
+  return n;
+}
+
+void PutMeta(Writer& w, const Meta& m) {
+  w.pod<int32_t>(m.head);
+  w.pod<int32_t>(m.app_id);
+  w.pod<int32_t>(m.customer_id);
+  w.pod<int32_t>(m.timestamp);
+  w.pod<int32_t>(m.sender);
+  w.pod<int32_t>(m.receiver);
+  w.pod<uint8_t>((uint8_t)(m.request | (m.push << 1) | (m.pull << 2) | (m.simple_app << 3)));
+  w.str(m.body);
+  w.pod<uint32_t>((uint32_t)m.data_type.size());
+  for (DataType t : m.data_type) w.pod<int32_t>((int32_t)t);
+  w.pod<int32_t>(m.control.cmd);
+  w.pod<uint32_t>((uint32_t)m.control.nodes.size());
+  for (const Node& n : m.control.nodes) PutNode(w, n);
+  w.pod<int32_t>(m.control.barrier_group);
+  w.pod<uint64_t>(m.control.msg_sig);
+  w.pod<int32_t>(m.data_size);
+  w.pod<int32_t>(m.priority);
+}
+
+Meta GetMeta(Reader& r) {
+  Meta m;
+  m.head = r.pod<int32_t>();
+  m.app_id = r.pod<int32_t>();
+  m.customer_id = r.pod<int32_t>();
+  m.timestamp = r.pod<int32_t>();
+  m.sender = r.pod<int32_t>();
+  m.receiver = r.pod<int32_t>();
+  const uint8_t f = r.pod<uint8_t>();
+  m.request = f & 1;
+  m.push = (f >> 1) & 1;
+  m.pull = (f >> 2) & 1;
+  m.simple_app = (f >> 3) & 1;
+  m.body = r.str();
+  const uint32_t nt = r.pod<uint32_t>();
+  for (uint32_t i = 0; i < nt; ++i) m.data_type.push_back((DataType)r.pod<int32_t>());
+  m.control.cmd = (Control::Command)r.pod<int32_t>();
+  const uint32_t nn = r.pod<uint32_t>();
+  for (uint32_t i = 0; i < nn; ++i) m.control.nodes.push_back(GetNode(r));
+  m.control.barrier_group = r.pod<int32_t>();
+  m.control.msg_sig = r.pod<uint64_t>();
+  m.data_size = r.pod<int32_t>();
+  m.priority = r.pod<int32_t>();
+  return m;
+}
+
+struct WireHeader {
+  uint32_t magic;
+  uint32_t meta_bytes;
+  uint32_t nframes;
+  uint32_t reserved;
+};
+
+// kPeerFrame: a slice of an HBM frame the RECEIVER sent earlier and this node
+// mapped (a reply that echoes the request's keys, KVApp.h:449-455): sent back
+// as (token, offset) and resolved to the receiver's own array.
+enum FrameKind : uint8_t { kHostFrame = 0, kIpcFrame = 1, kPeerFrame = 2 };
+
+struct PeerFrame {
+  uint64_t token;
+  uint64_t offset;
+};
+
+struct IpcFrame {  // follows the frame's kind + size for kIpcFrame
+  char handle[kHandleBytes];
+  uint64_t offset;
+  uint64_t token;
+  int32_t device;
+};
+
+// HBM frames of peers mapped into this process: the views (so a reply can
+// point back into its receiver's own array) and the RELEASE_FRAME queue their
+// last references fill.  Shared with the views' deleters, so it outlives the Van.
+struct FrameRegistry {
+  struct View {
+    uintptr_t end;
+    int owner;
+    uint64_t token;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uintptr_t, View> views;          // start -> view
+  std::vector<std::pair<int, uint64_t>> q;  // (owner node id, token) to release
+  bool closed = false;
+  void Add(const char* p, uint64_t bytes, int owner, uint64_t token) {
+    std::lock_guard<std::mutex> lk(mu);
+    views[(uintptr_t)p] = View{(uintptr_t)p + bytes, owner, token};
+  }
+  void Release(const char* p, int owner, uint64_t token) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      views.erase((uintptr_t)p);
+      if (closed) return;
+      q.emplace_back(owner, token);
+    }
+    cv.notify_one();
+  }
+  /* the mapped view of `owner` containing [p, p + bytes), if any */
+  bool Find(const char* p, uint64_t bytes, int owner, PeerFrame* out) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = views.upper_bound((uintptr_t)p);
+    if (it == views.begin()) return false;
+    --it;
+    const View& v = it->second;
+    if (v.owner != owner || (uintptr_t)p + bytes > v.end) return false;
+    out->token = v.token;
+    out->offset = (uint64_t)((uintptr_t)p - it->first);
+    return true;
+  }
+};
+
+struct Conn {
+  int fd = -1;
+  std::mutex mu;  // one writer at a time
+  ~Conn() {
+    if (fd >= 0) ::close(fd);
+  }
+};
+
+class TcpVan : public Van {
+ public:
+  explicit TcpVan(PostOffice* po) : Van(po), rel_(std::make_shared<FrameRegistry>()) {}
+  ~TcpVan() override { Stop(); }
+
+  void Start(int customer_id) override;
+  void Stop() override;
+  bool Barrier(int customer_id, int group) override;
+  void NoteStarted(int customer_id) override;
+  void NotifyAbort(const std::string& why) override;
+
+ protected:
+  int SendMsg(const Message& msg) override;
+
+ private:
+  void Listen(const std::string& host, int port);
+  void AcceptLoop();
+  void ReadLoop(int fd);
+  void ReleaseLoop();
+  void Dispatch(Message& msg);
+  void OnAddNode(const Message& msg);
+  void OnBarrier(const Message& msg);
+  std::shared_ptr<Conn> Connect(int id);
+  int Encode(const Message& msg, const Node& to, std::string* head, std::vector<SVector<char>>* host_frames);
+  SVector<char> MapFrame(int sender, const IpcFrame& f, uint64_t bytes);
+  void SendControl(int to, Control::Command cmd, int group = 0, int customer_id = 0, const std::string& body = "");
+  bool Abandoned() const { return cluster::Aborted(); }
+
+  bool is_scheduler_ = false;
+  std::string my_host_;
+  int listen_fd_ = -1;
+  std::atomic<bool> stopping_{false};
+  std::thread accept_thread_, release_thread_;
+  std::mutex readers_mu_;
+  std::vector<std::thread> readers_;
+  std::vector<int> reader_fds_;
+
+  std::mutex peers_mu_;
+  std::map<int, Node> nodes_;                    // id -> address (scheduler: from the config)
+  std::map<int, std::shared_ptr<Conn>> conns_;  // id -> outgoing connection
+  std::set<int> terminated_;                    // peers that said goodbye
+
+  std::mutex reg_mu_;
+  std::condition_variable reg_cv_;
+  bool registered_ = false;
+  std::vector<Node> joined_;  // scheduler: ADD_NODE requests so far
+
+  std::mutex bar_mu_;
+  std::condition_variable bar_cv_;
+  std::map<std::pair<int, int>, uint64_t> bar_gen_;  // (group, customer) -> releases seen
+  std::map<std::pair<int, int>, int> bar_count_;     // scheduler: arrivals
+  std::map<int, std::set<int>> started_;             // scheduler: customer -> node ids
+
+  std::mutex frames_mu_;
+  uint64_t next_token_ = 1;
+  std::unordered_map<uint64_t, SVector<char>> inflight_;  // frames peers have mapped
+  std::map<std::pair<int, std::string>, char*> mapped_;   // (owner, handle) -> base
+  std::shared_ptr<FrameRegistry> rel_;
+  std::atomic<bool> abort_sent_{false};
+  bool started_van_ = false;
+};
+
+// ---------------------------------------------------------------------------
+void TcpVan::Listen(const std::string& host, int port) {
+  listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+  CHECK_GE(listen_fd_, 0) << "socket: " << std::strerror(errno);
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in sa;
+  CHECK(Resolve(host, port, &sa)) << "cannot resolve " << host;
+  CHECK_EQ(::bind(listen_fd_, (sockaddr*)&sa, sizeof(sa)), 0)
+      << "bind " << host << ":" << port << ": " << std::strerror(errno);
+  CHECK_EQ(::listen(listen_fd_, 128), 0) << "listen: " << std::strerror(errno);
+  socklen_t len = sizeof(sa);
+  getsockname(listen_fd_, (sockaddr*)&sa, &len);
+  my_node_.hostname = host;
+  my_node_.port = ntohs(sa.sin_port);
+  accept_thread_ = std::thread([this] { AcceptLoop(); });
+}
+
+void TcpVan::AcceptLoop() {
+  while (!stopping_) {
+    int fd = ::accept(listen_fd_, nullptr, nullptr);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      return;  // listening socket shut down
+    }
+    Tune(fd);
+    std::lock_guard<std::mutex> lk(readers_mu_);
+    reader_fds_.push_back(fd);
+    readers_.emplace_back([this, fd] { ReadLoop(fd); });
+  }
+}
+
+void TcpVan::Start(int customer_id) {
+  (void)customer_id;
+  if (started_van_) return;
+  started_van_ = true;
+  is_scheduler_ = po_->is_scheduler();
+  my_host_ = Environment::GetOrDefault("PS_NODE_HOST", "127.0.0.1");
+  const std::string sched_host = Environment::GetOrDefault("PS_SCHEDULER_URI", "127.0.0.1");
+  const int sched_port = Environment::GetIntOrDefault("PS_SCHEDULER_PORT", 8000);
+  const int timeout_s = Environment::GetIntOrDefault("PS_REGISTER_TIMEOUT", 120);
+  Node sched;
+  sched.role = Node::SCHEDULER;
+  sched.id = kScheduler;
+  sched.hostname = sched_host;
+  sched.port = sched_port;
+  {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    nodes_[kScheduler] = sched;
+  }
+  release_thread_ = std::thread([this] { ReleaseLoop(); });
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+  if (is_scheduler_) {
+    my_node_ = sched;
+    Listen(sched_host, sched_port);
+    const size_t expect = (size_t)(po_->num_servers() + po_->num_workers());
+    std::vector<Node> joined;
+    {
+      std::unique_lock<std::mutex> lk(reg_mu_);
+      CHECK(reg_cv_.wait_until(lk, deadline, [&] { return joined_.size() >= expect || Abandoned(); }))
+          << "scheduler: " << joined_.size() << " of " << expect << " nodes registered in " << timeout_s << " s";
+      joined = joined_;
+    }
+    CHECK(!Abandoned()) << "job aborted during registration: " << cluster::AbortReason();
+    // ranks in address order (Van.cpp:292-296)
+    std::sort(joined.begin(), joined.end(), [](const Node& a, const Node& b) {
+      int c = a.hostname.compare(b.hostname);
+      return c != 0 ? c > 0 : a.port < b.port;
+    });
+    int ns = 0, nw = 0;
+    for (Node& n : joined) n.id = n.role == Node::SERVER ? PostOffice::ServerRankToID(ns++) : PostOffice::WorkerRankToID(nw++);
+    CHECK_EQ(ns, po_->num_servers()) << "registered servers";
+    CHECK_EQ(nw, po_->num_workers()) << "registered workers";
+    joined.push_back(my_node_);
+    {
+      std::lock_guard<std::mutex> lk(peers_mu_);
+      for (const Node& n : joined) nodes_[n.id] = n;
+    }
+    Message table;
+    table.meta.control.cmd = Control::ADD_NODE;
+    table.meta.control.nodes = joined;
+    for (const Node& n : joined) {
+      if (n.id == kScheduler) continue;
+      table.meta.receiver = n.id;
+      table.meta.timestamp = GetAvailableTimestamp();
+      Send(table);
+    }
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    registered_ = true;
+  } else {
+    Listen(my_host_, 0);
+    my_node_.role = po_->role();
+    my_node_.id = Node::kEmpty;
+    my_node_.gpu = device::Count() > 0;
+    // the scheduler may start after us (local.py starts them in order, but
+    // nothing waits): retry the first connection until the deadline
+    std::shared_ptr<Conn> c;
+    while (!(c = Connect(kScheduler))) {
+      CHECK(std::chrono::steady_clock::now() < deadline)
+          << "cannot reach the scheduler at " << sched_host << ":" << sched_port;
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    Message join;
+    join.meta.control.cmd = Control::ADD_NODE;
+    join.meta.request = true;
+    join.meta.receiver = kScheduler;
+    join.meta.control.nodes.push_back(my_node_);
+    CHECK_NE(SendMsg(join), -1) << "ADD_NODE to the scheduler failed";
+    std::unique_lock<std::mutex> lk(reg_mu_);
+    CHECK(reg_cv_.wait_until(lk, deadline, [&] { return registered_ || Abandoned(); }))
+        << "no node table from the scheduler in " << timeout_s << " s";
+    CHECK(!Abandoned()) << "job aborted during registration: " << cluster::AbortReason();
+  }
+  ready_ = true;
+}
+
+void TcpVan::OnAddNode(const Message& msg) {
+  if (msg.meta.request) {  // at the scheduler
+    CHECK(is_scheduler_) << "ADD_NODE request at a non-scheduler";
+    CHECK_EQ(msg.meta.control.nodes.size(), (size_t)1);
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    joined_.push_back(msg.meta.control.nodes[0]);
+    reg_cv_.notify_all();
+    return;
+  }
+  // the node table (Van.cpp:404-431)
+  int my_rank = -1;
+  {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    for (const Node& n : msg.meta.control.nodes) {
+      nodes_[n.id] = n;
+      if (n.hostname == my_node_.hostname && n.port == my_node_.port) {
+        my_node_.id = n.id;
+        my_rank = PostOffice::IDToRank(n.id);
+      }
+    }
+  }
+  CHECK_GE(my_rank, 0) << "this node is missing from the scheduler's table";
+  const int ndev = device::Count();
+  po_->SetIdentity(my_rank, ndev > 0 ? my_rank % ndev : -1);
+  std::lock_guard<std::mutex> lk(reg_mu_);
+  registered_ = true;
+  reg_cv_.notify_all();
+}
+
+void TcpVan::OnBarrier(const Message& msg) {
+  const int group = msg.meta.control.barrier_group;
+  const int cid = msg.meta.customer_id;
+  const auto key = std::make_pair(group, cid);
+  if (!msg.meta.request) {  // release
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    ++bar_gen_[key];
+    bar_cv_.notify_all();
+    return;
+  }
+  CHECK(is_scheduler_) << "BARRIER request at a non-scheduler";
+  std::vector<int> release;
+  {
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    const auto& ids = po_->GetNodeIDs(group);
+    int participants = (int)ids.size();
+    if (cid != 0) {
+      participants = 0;
+      for (int id : ids) participants += started_[cid].count(id) ? 1 : 0;
+      participants = std::max(participants, 1);
+    }
+    if (++bar_count_[key] < participants) return;
+    bar_count_[key] = 0;
+    for (int id : ids)
+      if (cid == 0 || started_[cid].count(id)) release.push_back(id);
+    if (release.empty()) release.push_back(msg.meta.sender);
+  }
+  // the scheduler's own release last: once it returns from the barrier it may
+  // stop its Van, and every other member must have its release by then
+  std::stable_partition(release.begin(), release.end(), [](int id) { return id != kScheduler; });
+  for (int id : release) SendControl(id, Control::BARRIER, group, cid);
+}
+
+bool TcpVan::Barrier(int customer_id, int group) {
+  const auto key = std::make_pair(group, customer_id);
+  uint64_t gen;
+  {
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    gen = bar_gen_[key];
+  }
+  Message req;
+  req.meta.request = true;
+  req.meta.control.cmd = Control::BARRIER;
+  req.meta.control.barrier_group = group;
+  req.meta.customer_id = customer_id;
+  req.meta.receiver = kScheduler;
+  req.meta.timestamp = GetAvailableTimestamp();
+  Send(req);
+  std::unique_lock<std::mutex> lk(bar_mu_);
+  while (bar_gen_[key] == gen) {
+    bar_cv_.wait_for(lk, std::chrono::milliseconds(100));
+    if (Abandoned()) {
+      lk.unlock();
+      LOG(FATAL) << "barrier abandoned: " << cluster::AbortReason();
+    }
+  }
+  return true;
+}
+
+void TcpVan::NoteStarted(int customer_id) {
+  if (is_scheduler_) {
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    started_[customer_id].insert(kScheduler);
+    return;
+  }
+  SendControl(kScheduler, Control::STARTED, 0, customer_id);
+}
+
+void TcpVan::NotifyAbort(const std::string& why) {
+  if (abort_sent_.exchange(true)) return;
+  if (!started_van_) return;
+  if (is_scheduler_) {
+    std::vector<int> ids;
+    {
+      std::lock_guard<std::mutex> lk(peers_mu_);
+      for (auto& kv : nodes_)
+        if (kv.first != kScheduler) ids.push_back(kv.first);
+    }
+    for (int id : ids) SendControl(id, Control::ABORT, 0, 0, why);
+  } else {
+    SendControl(kScheduler, Control::ABORT, 0, 0, why);
+  }
+}
+
+void TcpVan::SendControl(int to, Control::Command cmd, int group, int customer_id, const std::string& body) {
+  Message m;
+  m.meta.control.cmd = cmd;
+  m.meta.control.barrier_group = group;
+  m.meta.customer_id = customer_id;
+  m.meta.body = body;
+  m.meta.receiver = to;
+  m.meta.request = false;
+  m.meta.sender = my_node_.id;
+  const int rc = SendMsg(m);
+  // control traffic to a peer that already left (a late RELEASE_FRAME, an
+  // ABORT racing an exit) is not an error
+  if (rc < 0 && cmd != Control::RELEASE_FRAME && cmd != Control::ABORT && cmd != Control::TERMINATE && !stopping_)
+    LOG(FATAL) << "control message to node " << to << " failed";
+}
+
+// ---------------------------------------------------------------------------
+std::shared_ptr<Conn> TcpVan::Connect(int id) {
+  Node n;
+  {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    auto it = conns_.find(id);
+    if (it != conns_.end()) return it->second;
+    auto nt = nodes_.find(id);
+    if (nt == nodes_.end()) return nullptr;
+    n = nt->second;
+  }
+  sockaddr_in sa;
+  if (!Resolve(n.hostname, n.port, &sa)) return nullptr;
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0) return nullptr;
+  if (::connect(fd, (sockaddr*)&sa, sizeof(sa)) != 0) {
+    ::close(fd);
+    return nullptr;
+  }
+  Tune(fd);
+  auto c = std::make_shared<Conn>();
+  c->fd = fd;
+  std::lock_guard<std::mutex> lk(peers_mu_);
+  auto ins = conns_.emplace(id, c);
+  return ins.first->second;  // a racing connect to the same peer: keep one
+}
+
+int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
+                   std::vector<SVector<char>>* host_frames) {
+  Writer meta;
+  PutMeta(meta, msg.meta);
+  Writer frames;
+  int bytes = 0;
+  const bool can_map = to.gpu && to.hostname == my_node_.hostname;
+  for (const SVector<char>& f : msg.data) {
+    PeerFrame pf;
+    if (f.on_device() && f.size() && rel_->Find(f.data(), f.size(), to.id, &pf)) {
+      frames.pod<uint8_t>(kPeerFrame);
+      frames.pod<uint64_t>(f.size());
+      frames.pod(pf);
+      bytes += (int)sizeof(pf);
+      continue;
+    }
+    if (f.on_device() && f.size() && can_map) {
+      IpcFrame d;
+      std::memset(&d, 0, sizeof(d));
+      if (psg_ipc_export_range(f.data(), d.handle, &d.offset) == PSG_OK) {
+        d.device = f.device();
+        {
+          std::lock_guard<std::mutex> lk(frames_mu_);
+          d.token = next_token_++;
+          inflight_[d.token] = f;
+        }
+        frames.pod<uint8_t>(kIpcFrame);
+        frames.pod<uint64_t>(f.size());
+        frames.pod(d);
+        bytes += (int)sizeof(d);
+        continue;
+      }
+      LOG(WARNING) << "hipIpc export of an HBM frame failed (" << psg_last_error() << "); sending its bytes";
+    }
+    SVector<char> h = f;
+    if (f.on_device() && f.size()) {
+      h = SVector<char>::Uninitialized(f.size());
+      device::CopySync(h.data(), f.data(), f.size(), 1);
+    }
+    frames.pod<uint8_t>(kHostFrame);
+    frames.pod<uint64_t>(h.size());
+    host_frames->push_back(h);
+    bytes += (int)h.size();
+  }
+  WireHeader wh{kMagic, (uint32_t)meta.b.size(), (uint32_t)msg.data.size(), 0};
+  head->assign(reinterpret_cast<const char*>(&wh), sizeof(wh));
+  head->append(meta.b);
+  head->append(frames.b);
+  return bytes + (int)head->size();
+}
+
+int TcpVan::SendMsg(const Message& msg) {
+  const int to = msg.meta.receiver;
+  if (to == my_node_.id && my_node_.id != Node::kEmpty) {  // to itself: no socket
+    Message m = msg;
+    Dispatch(m);
+    return (int)sizeof(Meta) + msg.meta.data_size;
+  }
+  std::shared_ptr<Conn> c = Connect(to);
+  if (!c) return -1;
+  Node dst;
+  {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    dst = nodes_[to];
+  }
+  std::string head;
+  std::vector<SVector<char>> host;
+  const int bytes = Encode(msg, dst, &head, &host);
+  std::lock_guard<std::mutex> lk(c->mu);
+  // frame descriptors precede the host frame payloads, in frame order
+  if (!WriteAll(c->fd, head.data(), head.size())) return -1;
+  for (const SVector<char>& h : host)
+    if (h.size() && !WriteAll(c->fd, h.data(), h.size())) return -1;
+  return bytes;
+}
+
+SVector<char> TcpVan::MapFrame(int sender, const IpcFrame& f, uint64_t bytes) {
+  const int dev = po_->device();
+  CHECK_GE(dev, 0) << "an HBM frame reached a node without a GPU";
+  device::Use(dev);
+  const auto key = std::make_pair(sender, std::string(f.handle, kHandleBytes));
+  char* base = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(frames_mu_);
+    auto it = mapped_.find(key);
+    if (it != mapped_.end()) base = it->second;
+  }
+  if (!base) {
+    void* p = nullptr;
+    device::Check(psg_ipc_open(f.handle, &p), "psg_ipc_open (HBM frame of a peer process)");
+    base = static_cast<char*>(p);
+    std::lock_guard<std::mutex> lk(frames_mu_);
+    mapped_.emplace(key, base);  // kept for the process lifetime (pooled blocks recur)
+  }
+  std::shared_ptr<FrameRegistry> reg = rel_;
+  const uint64_t token = f.token;
+  char* view = base + f.offset;
+  reg->Add(view, bytes, sender, token);
+  return SVector<char>(view, bytes, [reg, sender, token](char* p) { reg->Release(p, sender, token); }, f.device);
+}
+
+void TcpVan::ReadLoop(int fd) {
+  int peer = Node::kEmpty;
+  bool said_goodbye = false;
+  while (true) {
+    WireHeader wh;
+    if (!ReadAll(fd, &wh, sizeof(wh))) break;
+    if (wh.magic != kMagic) {
+      LOG(ERROR) << "bad frame header from node " << peer << "; closing the connection";
+      break;
+    }
+    std::string mb(wh.meta_bytes, '\0');
+    if (!ReadAll(fd, &mb[0], mb.size())) break;
+    Message msg;
+    try {
+      Reader r{mb.data(), mb.data() + mb.size()};
+      msg.meta = GetMeta(r);
+      peer = msg.meta.sender;
+      struct Pending {
+        uint8_t kind;
+        uint64_t bytes;
+        IpcFrame ipc;
+        PeerFrame peer;
+      };
+      std::vector<Pending> descs(wh.nframes);
+      bool ok = true;
+      for (auto& d : descs) {
+        ok = ok && ReadAll(fd, &d.kind, 1) && ReadAll(fd, &d.bytes, 8);
+        if (ok && d.kind == kIpcFrame) ok = ReadAll(fd, &d.ipc, sizeof(d.ipc));
+        if (ok && d.kind == kPeerFrame) ok = ReadAll(fd, &d.peer, sizeof(d.peer));
+      }
+      if (!ok) break;
+      for (auto& d : descs) {
+        if (d.kind == kHostFrame) {
+          SVector<char> h = SVector<char>::Uninitialized(d.bytes);
+          if (d.bytes && !ReadAll(fd, h.data(), d.bytes)) {
+            ok = false;
+            break;
+          }
+          msg.data.push_back(h);
+        } else if (d.kind == kPeerFrame) {  // our own frame, echoed
+          SVector<char> own;
+          {
+            std::lock_guard<std::mutex> lk(frames_mu_);
+            auto it = inflight_.find(d.peer.token);
+            CHECK(it != inflight_.end()) << "node " << peer << " echoed an HBM frame no longer in flight";
+            own = it->second;
+          }
+          msg.data.push_back(own.Slice(d.peer.offset, d.peer.offset + d.bytes));
+        } else {
+          msg.data.push_back(MapFrame(peer, d.ipc, d.bytes));
+        }
+      }
+      if (!ok) break;
+      if (msg.meta.control.cmd == Control::TERMINATE) said_goodbye = true;
+      Dispatch(msg);
+    } catch (const std::exception& e) {
+      cluster::Abort(std::string("receive from node ") + std::to_string(peer) + ": " + e.what());
+    }
+  }
+  if (!said_goodbye && !stopping_ && !cluster::Aborted() && peer != Node::kEmpty) {
+    bool known_gone;
+    {
+      std::lock_guard<std::mutex> lk(peers_mu_);
+      known_gone = terminated_.count(peer) > 0;
+    }
+    if (!known_gone) cluster::Abort("node " + std::to_string(peer) + " disconnected");
+  }
+}
+
+void TcpVan::Dispatch(Message& msg) {
+  switch (msg.meta.control.cmd) {
+    case Control::EMPTY:
+      CHECK_NE(msg.meta.app_id, Meta::kEmpty);
+      cluster::DeliverTo(po_, msg);
+      return;
+    case Control::ADD_NODE: OnAddNode(msg); return;
+    case Control::BARRIER: OnBarrier(msg); return;
+    case Control::STARTED: {
+      std::lock_guard<std::mutex> lk(bar_mu_);
+      started_[msg.meta.customer_id].insert(msg.meta.sender);
+      return;
+    }
+    case Control::RELEASE_FRAME: {
+      Reader r{msg.meta.body.data(), msg.meta.body.data() + msg.meta.body.size()};
+      std::vector<SVector<char>> drop;  // released outside the lock
+      std::lock_guard<std::mutex> lk(frames_mu_);
+      while (r.p < r.e) {
+        auto it = inflight_.find(r.pod<uint64_t>());
+        if (it != inflight_.end()) {
+          drop.push_back(std::move(it->second));
+          inflight_.erase(it);
+        }
+      }
+      return;
+    }
+    case Control::ABORT: {
+      const std::string why = msg.meta.body;
+      if (is_scheduler_) {
+        abort_sent_ = false;  // forward it to everyone else
+        NotifyAbort(why);
+      }
+      abort_sent_ = true;
+      cluster::Abort(why);
+      return;
+    }
+    case Control::TERMINATE: {
+      std::lock_guard<std::mutex> lk(peers_mu_);
+      terminated_.insert(msg.meta.sender);
+      return;
+    }
+    default: return;  // ACK / HEARTBEAT: not used in one host
+  }
+}
+
+void TcpVan::ReleaseLoop() {
+  std::shared_ptr<FrameRegistry> rq = rel_;
+  while (true) {
+    std::vector<std::pair<int, uint64_t>> batch;
+    {
+      std::unique_lock<std::mutex> lk(rq->mu);
+      rq->cv.wait(lk, [&] { return rq->closed || !rq->q.empty(); });
+      if (rq->q.empty() && rq->closed) return;
+      batch.swap(rq->q);
+    }
+    std::map<int, Writer> by_owner;
+    for (auto& t : batch) by_owner[t.first].pod<uint64_t>(t.second);
+    for (auto& kv : by_owner) SendControl(kv.first, Control::RELEASE_FRAME, 0, 0, kv.second.b);
+  }
+}
+
+void TcpVan::Stop() {
+  if (!started_van_ || stopping_.exchange(true)) return;
+  ready_ = false;
+  {
+    std::lock_guard<std::mutex> lk(rel_->mu);
+    rel_->closed = true;
+  }
+  rel_->cv.notify_all();
+  if (release_thread_.joinable()) release_thread_.join();
+  std::map<int, std::shared_ptr<Conn>> conns;
+  {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    conns.swap(conns_);
+  }
+  for (auto& kv : conns) {  // goodbye: the peer's reader then expects the close
+    Message bye;
+    bye.meta.control.cmd = Control::TERMINATE;
+    bye.meta.sender = my_node_.id;
+    std::string head;
+    std::vector<SVector<char>> host;
+    Encode(bye, Node(), &head, &host);
+    std::lock_guard<std::mutex> lk(kv.second->mu);
+    WriteAll(kv.second->fd, head.data(), head.size());
+    ::shutdown(kv.second->fd, SHUT_RDWR);
+  }
+  if (listen_fd_ >= 0) {
+    ::shutdown(listen_fd_, SHUT_RDWR);
+    ::close(listen_fd_);
+  }
+  if (accept_thread_.joinable()) accept_thread_.join();
+  std::vector<std::thread> readers;
+  {
+    std::lock_guard<std::mutex> lk(readers_mu_);
+    for (int fd : reader_fds_) ::shutdown(fd, SHUT_RDWR);
+    readers.swap(readers_);
+  }
+  for (auto& t : readers) t.join();
+  {
+    std::lock_guard<std::mutex> lk(readers_mu_);
+    for (int fd : reader_fds_) ::close(fd);
+    reader_fds_.clear();
+  }
+  std::lock_guard<std::mutex> lk(frames_mu_);
+  inflight_.clear();
+}
+
+// ---------------------------------------------------------------------------
+PostOffice* g_node = nullptr;
+
+Node::Role ParseRole(const std::string& r) {
+  if (r == "scheduler") return Node::SCHEDULER;
+  if (r == "server") return Node::SERVER;
+  return Node::WORKER;
+}
+
+bool IsRole(const char* s) {
+  return s && (!std::strcmp(s, "scheduler") || !std::strcmp(s, "server") || !std::strcmp(s, "worker"));
+}
+
+}  // namespace
+
+Van* NewTcpVan(PostOffice* po) { return new TcpVan(po); }
+
+namespace proc {
+
+bool Active() { return g_node != nullptr; }
+PostOffice* Node() { return g_node; }
+
+const char* RoleOf(int argc, char** argv) {
+  if (argc >= 4 && IsRole(argv[3])) return argv[3];
+  const char* env = std::getenv("PS_ROLE");
+  if (IsRole(env) && argc >= 2 && argc <= 3) return env;
+  return nullptr;
+}
+
+int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** argv) {
+  const char* role = RoleOf(argc, argv);
+  CHECK(role) << "process mode needs a role (argv[3] or PS_ROLE)";
+  ReadLocalConfigToEnv(argv[1]);
+  const int ns = Environment::GetIntOrDefault("PS_NUM_SERVER", 1);
+  const int nw = Environment::GetIntOrDefault("PS_NUM_WORKER", 1);
+  const Node::Role r = ParseRole(role);
+  g_node = new PostOffice(r, r == Node::SCHEDULER ? 0 : -1, ns, nw, -1, "tcp");
+  g_node->BindThread();
+  int rc = 0;
+  try {
+    rc = node_main(argc, argv);
+  } catch (const std::exception& e) {
+    rc = 1;
+    cluster::Abort(std::string(role) + ": " + e.what());
+  }
+  if (cluster::Aborted()) rc = rc ? rc : 1;
+  g_node->van()->Stop();
+  // the node (and its Van's mapped frames) stays until exit: a program may still
+  // hold SVectors or a KVServer whose teardown runs in static destructors
+  return rc;
+}
+
+int Launch(int num_servers, int num_workers, int argc, char** argv) {
+  CHECK_GT(num_servers, 0);
+  CHECK_GT(num_workers, 0);
+  // a free port for the scheduler
+  int port = 0;
+  {
+    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in sa;
+    Resolve("127.0.0.1", 0, &sa);
+    CHECK_EQ(::bind(fd, (sockaddr*)&sa, sizeof(sa)), 0);
+    socklen_t len = sizeof(sa);
+    getsockname(fd, (sockaddr*)&sa, &len);
+    port = ntohs(sa.sin_port);
+    ::close(fd);
+  }
+  const char* tmp = std::getenv("TMPDIR");
+  std::string dir = std::string(tmp && *tmp ? tmp : "/tmp") + "/ps_procs_XXXXXX";
+  std::vector<char> dbuf(dir.begin(), dir.end());
+  dbuf.push_back(0);
+  CHECK(mkdtemp(dbuf.data())) << "mkdtemp " << dir;
+  dir = dbuf.data();
+  // per-role config files as local.py writes them (local.py:61-85)
+  auto cfg = [&](const char* role) {
+    std::string path = dir + "/config_" + role + ".json";
+    std::ofstream f(path);
+    f << "{\n  \"PS_NUM_SERVER\": " << num_servers << ",\n  \"PS_NUM_WORKER\": " << num_workers
+      << ",\n  \"PS_ROLE\": \"" << role << "\",\n  \"PS_SCHEDULER_URI\": \"127.0.0.1\",\n"
+      << "  \"PS_SCHEDULER_PORT\": " << port << ",\n  \"PS_VAN_TYPE\": \"tcp\"\n}\n";
+    return path;
+  };
+  char exe[4096];
+  ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+  CHECK_GT(n, 0) << "readlink /proc/self/exe";
+  exe[n] = 0;
+  std::vector<pid_t> pids;
+  std::vector<std::string> logs;
+  auto spawn = [&](const char* role, int i) {
+    std::vector<std::string> args = {argv[0], cfg(role), dir + "/log_" + role + std::to_string(i) + ".txt", role};
+    for (int k = 1; k < argc; ++k) args.push_back(argv[k]);
+    std::vector<char*> av;
+    for (auto& a : args) av.push_back(&a[0]);
+    av.push_back(nullptr);
+    pid_t pid;
+    int rc = posix_spawn(&pid, exe, nullptr, nullptr, av.data(), environ);
+    CHECK_EQ(rc, 0) << "posix_spawn " << exe << ": " << std::strerror(rc);
+    pids.push_back(pid);
+    logs.push_back(args[2]);
+  };
+  spawn("scheduler", 0);
+  for (int i = 0; i < num_servers; ++i) spawn("server", i);
+  for (int i = 0; i < num_workers; ++i) spawn("worker", i);
+  // wait; once a node failed, give the others (which get the ABORT) 30 s
+  int rc = 0;
+  size_t left = pids.size();
+  auto failed_at = std::chrono::steady_clock::time_point::max();
+  while (left) {
+    int status = 0;
+    pid_t p = waitpid(-1, &status, WNOHANG);
+    if (p > 0) {
+      --left;
+      const bool bad = !WIFEXITED(status) || WEXITSTATUS(status) != 0;
+      if (bad && !rc) {
+        rc = 1;
+        failed_at = std::chrono::steady_clock::now();
+      }
+      continue;
+    }
+    if (p < 0 && errno != EINTR) break;
+    if (rc && std::chrono::steady_clock::now() - failed_at > std::chrono::seconds(30)) {
+      for (pid_t q : pids) kill(q, SIGKILL);
+      failed_at = std::chrono::steady_clock::time_point::max();
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  for (const char* r : {"scheduler", "server", "worker"}) std::remove((dir + "/config_" + r + ".json").c_str());
+  if (!std::getenv("PS_KEEP_LOGS")) {
+    for (auto& l : logs) std::remove(l.c_str());
+    rmdir(dir.c_str());
+  }
+  return rc;
+}
+
+}  // namespace proc
+}  // namespace ps

@@ -22,8 +22,9 @@ class LocalVan : public Van {
 
 Van* Van::Create(const std::string& type, PostOffice* po) {
   if (type == "local" || type.empty()) return new LocalVan(po);
-  LOG(FATAL) << "PS_VAN_TYPE \"" << type << "\" is not available: this runtime keeps every node in one "
-             << "process per MI355X node (\"local\")";
+  if (type == "tcp") return NewTcpVan(po);
+  LOG(FATAL) << "PS_VAN_TYPE \"" << type << "\" is not available: \"local\" (every node a thread of "
+             << "one process) or \"tcp\" (one node per process)";
   return nullptr;
 }
 

@@ -85,3 +85,48 @@ def test_device_frames_end_to_end(ns, nw):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == nw
+
+
+# ---- process mode: one node per OS process (src/tcp_van.cc) -------------------
+# The launcher's -procs does what tests/local.py does: a scheduler, ns servers
+# and nw workers as separate processes that meet over TCP.  Host frames travel
+# on the sockets; HBM frames as hipIpc handles mapped in place by the receiver.
+
+@pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
+def test_reference_test_kv_app_processes(ns, nw):
+    exe = os.path.join(DROPIN, "test_kv_app")
+    _need(exe)
+    r = run(exe, "-ns", ns, "-nw", nw, "-procs")
+    assert r.returncode == 0, r.stderr[-3000:]
+    errs = re.findall(r"got error value: ([\d.eE+-]+), ([\d.eE+-]+)", r.stdout)
+    assert len(errs) == nw and all(float(a) == 0 and float(b) == 0 for a, b in errs), r.stdout
+
+
+def test_reference_multi_workers_processes():
+    exe = os.path.join(DROPIN, "test_kv_app_multi_workers")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 1, "-procs")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("got error value: 0, 0") == 2, r.stdout
+
+
+def test_reference_test_my_processes():
+    exe = os.path.join(DROPIN, "test_my")
+    _need(exe)
+    r = run(exe, "-ns", 1, "-nw", 1, "-procs")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("got error value") == 3
+
+
+@pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
+def test_device_frames_across_processes(ns, nw):
+    """ZPush / ZPull of HBM SVectors between processes: the server kernels read
+    the workers' keys and values through hipIpc mappings, the pull replies
+    (server HBM) are merged in place by the worker, and the echoed key frames
+    resolve to the worker's own arrays."""
+    exe = os.path.join(BIN, "kv_cluster_device")
+    _need(exe)
+    r = run(exe, "-ns", ns, "-nw", nw, "-procs", 200000, 20)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == nw

@@ -80,3 +80,82 @@ def test_default_handle_fails_loudly_without_gpu():
     r = run(exe, "-ns", 1, "-nw", 1, timeout=60)
     assert r.returncode != 0
     assert "value store lives in HBM" in r.stderr
+
+
+# ---- process mode: one node per OS process (src/tcp_van.cc) ------------------
+@pytest.mark.parametrize("ns,nw", [(1, 1), (2, 3)])
+def test_dropin_connection_processes(ns, nw):
+    exe = os.path.join(DROPIN, "test_connection")
+    _need(exe)
+    r = run(exe, "-ns", ns, "-nw", nw, "-procs")
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_dropin_simple_app_processes():
+    """test_simple_app.cpp counts requests in a process-global `num` and CHECKs
+    it equals 100 on every node: that holds only with one node per process."""
+    exe = os.path.join(DROPIN, "test_simple_app")
+    _need(exe)
+    for ns, nw in [(1, 1), (2, 2)]:
+        r = run(exe, "-ns", ns, "-nw", nw, "-procs")
+        assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("ns,nw", [(1, 1), (3, 2)])
+def test_host_cluster_processes(ns, nw):
+    exe = os.path.join(BIN, "kv_cluster_host")
+    _need(exe)
+    r = run(exe, "-ns", ns, "-nw", nw, "-procs")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count(" ok") == nw
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_localpy_style_launch(tmp_path):
+    """The launch protocol of tests/local.py (local.py:61-114), restated: one
+    JSON config per role (PS_NUM_SERVER, PS_NUM_WORKER, PS_ROLE,
+    PS_SCHEDULER_URI, PS_SCHEDULER_PORT) and one process per node started as
+    `prog config log role` — no launcher of ours involved."""
+    import json
+    exe = os.path.join(BIN, "kv_cluster_host")
+    _need(exe)
+    ns, nw, port = 2, 2, _free_port()
+    procs = []
+
+    def start(role, i):
+        cfg = tmp_path / f"config_{role}.json"
+        cfg.write_text(json.dumps({"PS_NUM_SERVER": ns, "PS_NUM_WORKER": nw, "PS_ROLE": role,
+                                   "PS_SCHEDULER_URI": "127.0.0.1", "PS_SCHEDULER_PORT": port,
+                                   "PS_VERBOSE": 1}, indent=4))
+        log = tmp_path / f"log_{role}{i}.txt"
+        procs.append(subprocess.Popen([exe, str(cfg), str(log), role], stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+
+    # local.py starts the scheduler first; start it LAST here, so the nodes
+    # must wait for it
+    for i in range(nw):
+        start("worker", i)
+    for i in range(ns):
+        start("server", i)
+    start("scheduler", 0)
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-1000:] for o in outs]
+    assert sum(o[0].count(" ok") for o in outs) == nw
+
+
+def test_process_job_fails_fast_on_a_failed_check():
+    """A CHECK that fails in one process (the HBM store on a host without a GPU)
+    is broadcast: every process ends, none waits on a barrier forever."""
+    exe = os.path.join(DROPIN, "test_kv_app")
+    _need(exe)
+    if _has_gpu():
+        pytest.skip("a GPU is present")
+    r = run(exe, "-ns", 2, "-nw", 2, "-procs", timeout=90)
+    assert r.returncode != 0
+    assert "value store lives in HBM" in r.stderr
