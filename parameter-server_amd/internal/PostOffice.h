@@ -52,6 +52,11 @@ class PostOffice {
 
   void RegisterExitCallback(const std::function<void()>& cb) { exit_callback_ = cb; }
   void Barrier(int customer_id, int node_group);
+  /* Every node of node_group calls it (like a barrier); each gets the bytes
+   * the group's root — its lowest node id — passed as `mine`.  The control
+   * plane's rendezvous for state a group shares, e.g. an RCCL unique id
+   * (ps::CreateComm). */
+  std::string GroupBroadcast(int node_group, const std::string& mine);
 
   static int ServerRankToID(int rank) { return rank * 2 + 8; }
   static int WorkerRankToID(int rank) { return rank * 2 + 9; }
@@ -113,6 +118,7 @@ PostOffice* NodeByArgv(char** argv);
 /* barrier of (group, customer_id) across the group's nodes */
 void Barrier(PostOffice* po, int customer_id, int group);
 void NoteStarted(PostOffice* po, int customer_id);
+std::string GroupBroadcast(PostOffice* po, int group, const std::string& mine);
 void Deliver(const Message& msg);
 /* hand msg to the right customer of node dst (Van.cpp:226-237) */
 void DeliverTo(PostOffice* dst, const Message& msg);

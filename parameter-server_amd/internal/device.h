@@ -35,6 +35,14 @@ void SliceKeys(const uint64_t* keys, size_t n, const int* lens, size_t num_vals,
 /* psg_merge on the thread stream, then synchronise */
 void Merge(std::vector<psg_segment>* segs, int elem_size, void* dst, uint64_t dst_count);
 
+/* An RCCL communicator (psg_comm) over the nodes of a ps group (kServerGroup,
+ * kWorkerGroup, ...): this node's rank is its position in
+ * PostOffice::GetNodeIDs(group).  The group's root (lowest node id) makes the
+ * RCCL unique id and the control plane hands it to every member
+ * (PostOffice::GroupBroadcast: through the scheduler in process mode).
+ * Collective: every member calls it; one GPU per member. */
+psg_comm* CreateComm(int group);
+
 /* psg dtype of a value type (-1 if the store does not support it) */
 template <typename V>
 constexpr int DType() {

@@ -48,10 +48,12 @@ struct Node {
 };
 
 struct Control {
-  // STARTED / RELEASE_FRAME / ABORT are this runtime's own (process mode,
-  // src/tcp_van.cc): a customer started; an HBM frame a peer mapped is no
-  // longer referenced; the job failed.
-  enum Command { EMPTY, TERMINATE, ADD_NODE, BARRIER, ACK, HEARTBEAT, STARTED, RELEASE_FRAME, ABORT };
+  // STARTED / RELEASE_FRAME / ABORT / GROUP_BCAST are this runtime's own
+  // (process mode, src/tcp_van.cc): a customer started; an HBM frame a peer
+  // mapped is no longer referenced; the job failed; a group rendezvous (the
+  // RCCL unique id of ps::CreateComm).
+  enum Command { EMPTY, TERMINATE, ADD_NODE, BARRIER, ACK, HEARTBEAT, STARTED, RELEASE_FRAME, ABORT,
+                 GROUP_BCAST };
   Command cmd = EMPTY;
   std::vector<Node> nodes;
   int barrier_group = 0;

@@ -44,6 +44,14 @@ class Van {
   virtual void NoteStarted(int customer_id) { (void)customer_id; }
   /* tell the other processes the job failed (their waiters then throw) */
   virtual void NotifyAbort(const std::string& why) { (void)why; }
+  /* process mode: every node of `group` calls it; all get the bytes the
+   * group's root (its lowest node id) passed.  Returns false on the local Van. */
+  virtual bool GroupBroadcast(int group, const std::string& mine, std::string* out) {
+    (void)group;
+    (void)mine;
+    (void)out;
+    return false;
+  }
   uint64_t send_bytes() const { return send_bytes_.load(); }
   uint64_t receive_bytes() const { return receive_bytes_.load(); }
   void CountReceived(uint64_t b) { receive_bytes_ += b; }

@@ -9,6 +9,7 @@
 #include <thread>
 #include <vector>
 
+#include "internal/PostOffice.h"
 #include "ps/log.h"
 #include "ps/svector.h"
 
@@ -169,6 +170,24 @@ void Merge(std::vector<psg_segment>* segs, int elem_size, void* dst, uint64_t ds
   psg_stream s = ThreadStream();
   Check(psg_merge(segs->data(), (int)segs->size(), elem_size, dst, dst_count, s), "psg_merge");
   Check(psg_stream_sync(s), "psg_stream_sync");
+}
+
+psg_comm* CreateComm(int group) {
+  PostOffice* po = PostOffice::Get();
+  const std::vector<int>& ids = po->GetNodeIDs(group);
+  auto me = std::find(ids.begin(), ids.end(), po->my_id());
+  CHECK(me != ids.end()) << "node " << po->my_id() << " is not in group " << group;
+  CHECK_GE(po->device(), 0) << "CreateComm: this node has no GPU";
+  std::string mine;
+  if (po->my_id() == *std::min_element(ids.begin(), ids.end())) {
+    mine.resize((size_t)psg_comm_id_bytes());
+    Check(psg_comm_get_id(&mine[0]), "psg_comm_get_id");
+  }
+  const std::string uid = po->GroupBroadcast(group, mine);
+  CHECK_EQ(uid.size(), (size_t)psg_comm_id_bytes()) << "RCCL id from the group's root";
+  psg_comm* c = nullptr;
+  Check(psg_comm_init(uid.data(), (int)ids.size(), (int)(me - ids.begin()), &c), "psg_comm_init");
+  return c;
 }
 
 }  // namespace device

@@ -29,6 +29,12 @@ struct ClusterState {
     int arrived = 0;
   };
   std::map<std::pair<int, int>, Bar> bars;  // (group, customer_id)
+  struct Bcast {
+    uint64_t gen = 0;
+    int arrived = 0;
+    std::string root_bytes, result;
+  };
+  std::map<int, Bcast> bcasts;  // group -> rendezvous
   std::map<int, std::set<int>> started;     // node id -> customer ids that called Start
   bool configured = false;
   bool env_loaded = false;
@@ -117,6 +123,35 @@ void Barrier(PostOffice* po, int customer_id, int group) {
       LOG(FATAL) << "barrier abandoned: " << why;
     }
   }
+}
+
+std::string GroupBroadcast(PostOffice* po, int group, const std::string& mine) {
+  const auto& ids = po->GetNodeIDs(group);
+  const int root = *std::min_element(ids.begin(), ids.end());
+  if (ids.size() <= 1) return mine;
+  std::string out;
+  if (po->van()->GroupBroadcast(group, mine, &out)) return out;  // process mode
+  ClusterState& s = S();
+  std::unique_lock<std::mutex> lk(s.mu);
+  auto& b = s.bcasts[group];
+  if (po->my_id() == root) b.root_bytes = mine;
+  const uint64_t gen = b.gen;
+  if (++b.arrived >= (int)ids.size()) {
+    b.arrived = 0;
+    b.result = b.root_bytes;
+    ++b.gen;
+    s.cv.notify_all();
+    return b.result;
+  }
+  while (b.gen == gen) {
+    s.cv.wait_for(lk, std::chrono::milliseconds(100));
+    if (s.aborted) {
+      std::string why = s.why;
+      lk.unlock();
+      LOG(FATAL) << "group broadcast abandoned: " << why;
+    }
+  }
+  return b.result;
 }
 
 void Deliver(const Message& msg) {
@@ -295,6 +330,10 @@ const std::vector<Range>& PostOffice::GetServerRanges() {
   return server_key_ranges_;
 }
 
+std::string PostOffice::GroupBroadcast(int node_group, const std::string& mine) {
+  return cluster::GroupBroadcast(this, node_group, mine);
+}
+
 void PostOffice::Barrier(int customer_id, int node_group) {
   switch (role_) {
     case Node::SERVER: CHECK(node_group & kServerGroup); break;
@@ -318,6 +357,7 @@ int RunLocalCluster(int num_servers, int num_workers, const std::function<int(in
     s.why.clear();
     s.env_loaded = false;
     s.bars.clear();
+    s.bcasts.clear();
     s.started.clear();
     s.by_argv.clear();
   }

@@ -287,6 +287,7 @@ class TcpVan : public Van {
   bool Barrier(int customer_id, int group) override;
   void NoteStarted(int customer_id) override;
   void NotifyAbort(const std::string& why) override;
+  bool GroupBroadcast(int group, const std::string& mine, std::string* out) override;
 
  protected:
   int SendMsg(const Message& msg) override;
@@ -299,6 +300,7 @@ class TcpVan : public Van {
   void Dispatch(Message& msg);
   void OnAddNode(const Message& msg);
   void OnBarrier(const Message& msg);
+  void OnGroupBroadcast(const Message& msg);
   std::shared_ptr<Conn> Connect(int id);
   int Encode(const Message& msg, const Node& to, std::string* head, std::vector<SVector<char>>* host_frames);
   SVector<char> MapFrame(int sender, const IpcFrame& f, uint64_t bytes);
@@ -329,6 +331,12 @@ class TcpVan : public Van {
   std::map<std::pair<int, int>, uint64_t> bar_gen_;  // (group, customer) -> releases seen
   std::map<std::pair<int, int>, int> bar_count_;     // scheduler: arrivals
   std::map<int, std::set<int>> started_;             // scheduler: customer -> node ids
+  struct Bcast {
+    uint64_t gen = 0;    // results seen (node side)
+    int arrived = 0;     // scheduler side
+    std::string root_bytes, result;
+  };
+  std::map<int, Bcast> bcasts_;  // group -> rendezvous
 
   std::mutex frames_mu_;
   uint64_t next_token_ = 1;
@@ -515,6 +523,71 @@ void TcpVan::OnBarrier(const Message& msg) {
   // stop its Van, and every other member must have its release by then
   std::stable_partition(release.begin(), release.end(), [](int id) { return id != kScheduler; });
   for (int id : release) SendControl(id, Control::BARRIER, group, cid);
+}
+
+void TcpVan::OnGroupBroadcast(const Message& msg) {
+  const int group = msg.meta.control.barrier_group;
+  if (!msg.meta.request) {  // the root's bytes, from the scheduler
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    Bcast& b = bcasts_[group];
+    b.result = msg.meta.body;
+    ++b.gen;
+    bar_cv_.notify_all();
+    return;
+  }
+  CHECK(is_scheduler_) << "GROUP_BCAST request at a non-scheduler";
+  std::vector<int> members;
+  std::string bytes;
+  {
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    const auto& ids = po_->GetNodeIDs(group);
+    Bcast& b = bcasts_[group];
+    if (msg.meta.control.msg_sig) b.root_bytes = msg.meta.body;  // from the root
+    if (++b.arrived < (int)ids.size()) return;
+    b.arrived = 0;
+    bytes = b.root_bytes;
+    members.assign(ids.begin(), ids.end());
+  }
+  std::stable_partition(members.begin(), members.end(), [](int id) { return id != kScheduler; });
+  for (int id : members) {
+    Message m;
+    m.meta.control.cmd = Control::GROUP_BCAST;
+    m.meta.control.barrier_group = group;
+    m.meta.body = bytes;
+    m.meta.receiver = id;
+    m.meta.request = false;
+    m.meta.sender = my_node_.id;
+    CHECK_NE(SendMsg(m), -1) << "group broadcast to node " << id << " failed";
+  }
+}
+
+bool TcpVan::GroupBroadcast(int group, const std::string& mine, std::string* out) {
+  const auto& ids = po_->GetNodeIDs(group);
+  const bool root = my_node_.id == *std::min_element(ids.begin(), ids.end());
+  uint64_t gen;
+  {
+    std::lock_guard<std::mutex> lk(bar_mu_);
+    gen = bcasts_[group].gen;
+  }
+  Message req;
+  req.meta.request = true;
+  req.meta.control.cmd = Control::GROUP_BCAST;
+  req.meta.control.barrier_group = group;
+  req.meta.control.msg_sig = root ? 1 : 0;
+  if (root) req.meta.body = mine;
+  req.meta.receiver = kScheduler;
+  req.meta.timestamp = GetAvailableTimestamp();
+  Send(req);
+  std::unique_lock<std::mutex> lk(bar_mu_);
+  while (bcasts_[group].gen == gen) {
+    bar_cv_.wait_for(lk, std::chrono::milliseconds(100));
+    if (Abandoned()) {
+      lk.unlock();
+      LOG(FATAL) << "group broadcast abandoned: " << cluster::AbortReason();
+    }
+  }
+  *out = bcasts_[group].result;
+  return true;
 }
 
 bool TcpVan::Barrier(int customer_id, int group) {
@@ -789,6 +862,7 @@ void TcpVan::Dispatch(Message& msg) {
       return;
     case Control::ADD_NODE: OnAddNode(msg); return;
     case Control::BARRIER: OnBarrier(msg); return;
+    case Control::GROUP_BCAST: OnGroupBroadcast(msg); return;
     case Control::STARTED: {
       std::lock_guard<std::mutex> lk(bar_mu_);
       started_[msg.meta.customer_id].insert(msg.meta.sender);

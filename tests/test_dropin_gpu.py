@@ -22,8 +22,10 @@ DROPIN = os.path.join(ROOT, "tests", "_dropin")
 BIN = os.path.join(ROOT, "tests", "_bin")
 
 
-def run(path, *args, timeout=300):
-    return subprocess.run([path, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+def run(path, *args, timeout=300, env=None):
+    e = dict(os.environ, **(env or {}))
+    return subprocess.run([path, *map(str, args)], capture_output=True, text=True, timeout=timeout,
+                          env=e)
 
 
 def _need(path):
@@ -130,3 +132,16 @@ def test_device_frames_across_processes(ns, nw):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == nw
+
+
+@pytest.mark.parametrize("procs", [False, True])
+def test_rccl_comm_through_the_control_plane(procs):
+    """device::CreateComm: the servers' RCCL id travels through the scheduler
+    (PostOffice::GroupBroadcast), then a BSP Push + Pull runs over the
+    communicator (collectives forced even with one rank, so RCCL executes)."""
+    exe = os.path.join(BIN, "comm_group")
+    _need(exe)
+    args = ["-ns", 1, "-nw", 1] + (["-procs"] if procs else []) + ["comm"]
+    r = run(exe, *args, env={"PSG_COMM_FORCE_COLLECTIVE": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "comm ok" in r.stdout and r.stdout.count("bcast ok") == 3

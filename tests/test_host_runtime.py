@@ -159,3 +159,15 @@ def test_process_job_fails_fast_on_a_failed_check():
     r = run(exe, "-ns", 2, "-nw", 2, "-procs", timeout=90)
     assert r.returncode != 0
     assert "value store lives in HBM" in r.stderr
+
+
+@pytest.mark.parametrize("procs", [False, True])
+def test_group_broadcast(procs):
+    """PostOffice::GroupBroadcast (the rendezvous ps::CreateComm hands the RCCL
+    id through): every member of three groups gets its root's bytes, three
+    rounds, in thread mode and through the scheduler in process mode."""
+    exe = os.path.join(BIN, "comm_group")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 3, *(["-procs"] if procs else []))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("bcast ok") == 6
