@@ -171,3 +171,23 @@ def test_group_broadcast(procs):
     r = run(exe, "-ns", 2, "-nw", 3, *(["-procs"] if procs else []))
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.count("bcast ok") == 6
+
+
+REF_LOCAL_PY = "/root/reference/tests/local.py"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LOCAL_PY), reason="reference tree absent (GPU box)")
+def test_reference_local_py_launches_our_binaries(tmp_path):
+    """The reference's own launcher (tests/local.py, run where the reference
+    tree exists) starts our binaries unchanged: its `config log role` command
+    lines select process mode.  local.py ignores its children's exit codes, so
+    the check is on what the nodes print."""
+    import sys
+    for exe, expect in [(os.path.join(BIN, "kv_cluster_host"), 2),
+                        (os.path.join(DROPIN, "test_simple_app"), 0)]:
+        _need(exe)
+        r = subprocess.run([sys.executable, REF_LOCAL_PY, "-ns", "2", "-nw", "2", "-exec", exe],
+                           cwd=tmp_path, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "Check failed" not in r.stderr and "aborted" not in r.stderr, r.stderr[-2000:]
+        assert r.stdout.count(" ok") == expect, r.stdout
