@@ -46,9 +46,9 @@ WORKLOADS = {
     "keyed": ("f32", 4, 10_000_000, "configs[3]"),
 }
 # algorithmic HBM bytes per key of one keyed Push on the SORTED store:
-# request key 8 + store key 8 (resolve) + slot write 4 + slot read 4 + value 4
-# + store value read/write 8
-KEYED_PUSH_BYTES = 36
+# request key 8 + store key 8 (resolve) + value 4 + store value read/write 8
+# (the resolve is fused with the apply: no slot array goes to HBM and back)
+KEYED_PUSH_BYTES = 28
 
 
 class GpuBackend:
@@ -446,8 +446,8 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
             res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
     if world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
-                                   "SORTED-store Push: psg_slice + k_tile_windows + k_resolve + "
-                                   "k_slots (one host sync)", vb)
+                                   "SORTED-store Push: k_tile_windows + k_resolve_apply "
+                                   "(one host sync)", vb)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
                                    "k_dense_vec<PUSH> (store += vals)", vb)

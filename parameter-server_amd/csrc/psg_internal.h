@@ -139,8 +139,8 @@ struct psg_store {
   uint32_t* slots2;  // slots after an insert (second resolve)
   uint64_t* wlo;     // per-tile store-key windows of the resolve
   uint64_t slots_cap;
-  int* flags;        // device int[4]: missing count, contiguous flag, ...
-  int* flags_host;   // pinned mirror
+  int* flags;        // device view of flags_host: the kernels raise flags there
+  int* flags_host;   // pinned host int[4]: any key absent / non-contiguous / out of range / unsorted
 };
 
 namespace psg {

@@ -19,6 +19,7 @@
 //           the `operator[]` insert of KVApp.h:449/452 — by a parallel merge of
 //           the (compacted, sorted) new keys into K and V.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "psg_internal.h"
@@ -28,7 +29,15 @@ namespace psg {
 constexpr int kTile = 1024;  // request keys per block tile (4 per lane)
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
+// Request flags live in pinned host memory that the kernels write directly
+// (one plain store of 1 per wave that saw the condition — idempotent, no
+// atomics), so a request needs no flag reset launch and no flag copy: the
+// host zeroes them before the launch and reads them after the stream sync.
 enum { F_MISSING = 0, F_NONCONTIG = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
+
+__device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
+  if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
+}
 
 __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__ a, uint64_t lo,
                                                     uint64_t hi, uint64_t key) {
@@ -169,11 +178,130 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
     }
     __syncthreads();
   }
-  // one atomic per wave per flag (the compiler aggregates uniform adds)
-  if (missing) atomicAdd(&flags[F_MISSING], missing);
-  if (noncontig) atomicOr(&flags[F_NONCONTIG], 1);
-  if (range) atomicOr(&flags[F_RANGE], 1);
-  if (unsorted) atomicOr(&flags[F_UNSORTED], 1);
+  raise_flag(flags, F_MISSING, missing != 0);
+  raise_flag(flags, F_NONCONTIG, noncontig != 0);
+  raise_flag(flags, F_RANGE, range != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
+}
+
+// Pass 2, fused with the request: k_resolve's search, then each lane applies
+// the request to its (up to) 4 keys right away — store[slot] += val and/or
+// out[i] = store[slot] — so the slots never go to HBM and back (28 B/key
+// instead of 36: request key 8 + store key 8 + value 4 + store value 8).  An
+// absent key is skipped (a pull reads 0, what its insertion gives); the flags
+// tell the host to insert it and apply the request to it afterwards.
+template <int DT, int OP>
+__global__ __launch_bounds__(256) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
+                                                       const uint64_t* __restrict__ K, uint64_t S,
+                                                       const uint64_t* __restrict__ wlo, uint64_t kb,
+                                                       uint64_t ke,
+                                                       typename Elem<DT>::T* __restrict__ V,
+                                                       const typename Elem<DT>::T* __restrict__ vals,
+                                                       typename Elem<DT>::T* __restrict__ outv,
+                                                       int* __restrict__ flags, int vec) {
+  using E = Elem<DT>;
+  using T = typename E::T;
+  __shared__ uint64_t sK[kWin];
+  int missing = 0, range = 0, unsorted = 0;
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * kTile;
+    const uint64_t t1 = (t0 + kTile < n) ? t0 + kTile : n;
+    const uint64_t lo = wlo[tile];
+    uint64_t hi = tile + 1 < ntiles ? wlo[tile + 1] + 1 : wlo[ntiles];
+    if (hi > S) hi = S;
+    if (hi < lo) hi = lo;  // unsorted input
+    const uint64_t W = hi - lo;
+    const bool staged = W <= (uint64_t)kWin;
+    if (staged)
+      for (uint64_t j = threadIdx.x; j < W; j += kBlock) sK[j] = K[lo + j];
+    __syncthreads();
+    const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
+    uint64_t prev = i0 > 0 && i0 < t1 ? q[i0 - 1] : 0;
+    uint32_t r = 0;
+    uint64_t slot[kPerLane];
+    bool hit[kPerLane];
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      const uint64_t i = i0 + k;
+      hit[k] = false;
+      slot[k] = 0;
+      if (i >= t1) continue;
+      const uint64_t key = q[i];
+      if (key < kb || key >= ke) range = 1;
+      if (i > 0 && prev >= key) unsorted = 1;
+      prev = key;
+      uint64_t p;
+      bool found;
+      if (staged) {
+        const uint32_t w = (uint32_t)W;
+        if (k == 0) {
+          r = lower_bound_lds(sK, w, key);
+        } else if (!(r < w && sK[r] >= key)) {
+          if (r + 1 < w && sK[r + 1] >= key) r = r + 1;
+          else r = (r + 1 >= w) ? w : r + 1 + lower_bound_lds(sK + r + 1, w - r - 1, key);
+        }
+        p = lo + r;
+        found = r < w && sK[r] == key;
+      } else {
+        p = lower_bound_dev(K, lo, hi, key);
+        found = p < S && K[p] == key;
+      }
+      hit[k] = found;
+      slot[k] = p;
+      if (!found) missing++;
+    }
+    // apply: the 4 request values / replies of a lane are one 16-B vector
+    // when T is 4 B, the tile is whole and the caller's arrays are 16-B
+    // aligned (vec, checked on the host)
+    T v[kPerLane], o[kPerLane];
+    const bool whole = i0 + kPerLane <= t1;
+    if constexpr ((OP & PSG_PUSH) != 0) {
+      if constexpr (sizeof(T) == 4) {
+        if (whole && vec) {
+          const f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(vals + i0));
+#pragma unroll
+          for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < kPerLane; ++k) v[k] = (i0 + k < t1) ? vals[i0 + k] : (T)0.0f;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) v[k] = (i0 + k < t1) ? vals[i0 + k] : (T)0.0f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      T x = (T)0.0f;
+      if (hit[k]) {
+        x = V[slot[k]];
+        if constexpr ((OP & PSG_PUSH) != 0) {
+          x = E::add1(x, v[k]);
+          V[slot[k]] = x;
+        }
+      }
+      o[k] = x;
+    }
+    if constexpr ((OP & PSG_PULL) != 0) {
+      bool done = false;
+      if constexpr (sizeof(T) == 4) {
+        if (whole && vec) {
+          *reinterpret_cast<u32x4*>(outv + i0) = __builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]});
+          done = true;
+        }
+      }
+      if (!done) {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k)
+          if (i0 + k < t1) outv[i0 + k] = o[k];
+      }
+    }
+    __syncthreads();
+  }
+  raise_flag(flags, F_MISSING, missing != 0);
+  raise_flag(flags, F_RANGE, range != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
 
 // Block-wide exclusive scan helper over 256 lanes (wave = 64).
@@ -230,6 +358,7 @@ __global__ __launch_bounds__(256) void k_scan_counts(uint32_t* __restrict__ coun
     if (threadIdx.x == 0) carry += tot;
     __syncthreads();
   }
+  if (threadIdx.x == 0) counts[ntiles] = carry;  // the total: keys absent
 }
 
 // Pass 2: write the absent keys, in order, to miss[].
@@ -310,8 +439,8 @@ __global__ __launch_bounds__(256) void k_dense_keyed(typename Elem<DT>::T* __res
     }
     if constexpr ((OP & PSG_PULL) != 0) out[i] = s;
   }
-  if (bad) atomicOr(&flags[F_RANGE], 1);
-  if (unsorted) atomicOr(&flags[F_UNSORTED], 1);
+  raise_flag(flags, F_RANGE, bad != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
 
 // Slots of a DENSE store: key - key_begin (kNoSlot when outside).
@@ -329,9 +458,13 @@ __global__ __launch_bounds__(256) void k_dense_slots(const uint64_t* __restrict_
     if (!ok) bad = 1;
     slots[i] = ok ? (uint32_t)p : kNoSlot;
   }
-  if (bad) atomicOr(&flags[F_RANGE], 1);
-  if (unsorted) atomicOr(&flags[F_UNSORTED], 1);
+  raise_flag(flags, F_RANGE, bad != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
+
+// zero the request flags (host memory) before a flag-raising launch; the
+// previous request on this store has synchronised its stream
+static void reset_flags(psg_store* s) { memset(s->flags_host, 0, F_NFLAGS * sizeof(int)); }
 
 static unsigned grid_n(uint64_t n, uint64_t per_block) {
   uint64_t b = (n + per_block - 1) / per_block;
@@ -360,7 +493,7 @@ static int ensure_slots(psg_store* s, uint64_t n) {
 static int launch_resolve(psg_store* s, const uint64_t* q, uint64_t n, uint32_t* slots,
                           hipStream_t st) {
   const uint64_t ntiles = (n + kTile - 1) / kTile;
-  PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+  reset_flags(s);
   k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
   k_resolve<<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
                                                   s->key_end, slots, s->flags);
@@ -421,8 +554,7 @@ static int run_fixup(psg_store* s, int op, const void* vals, void* out, uint64_t
 }
 
 static int read_flags(psg_store* s, hipStream_t st) {
-  PSG_HIP(hipMemcpyAsync(s->flags_host, s->flags, F_NFLAGS * sizeof(int), hipMemcpyDeviceToHost, st));
-  PSG_HIP(hipStreamSynchronize(st));
+  PSG_HIP(hipStreamSynchronize(st));  // the kernels wrote flags_host directly
   return PSG_OK;
 }
 
@@ -452,14 +584,22 @@ static int merge_insert(psg_store* s, const uint64_t* miss, uint64_t m, hipStrea
   return PSG_OK;
 }
 
-static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, uint64_t m, hipStream_t st) {
+static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, hipStream_t st) {
   const uint64_t ntiles = (n + kTile - 1) / kTile;
   uint32_t* counts = nullptr;
   uint64_t* miss = nullptr;
-  PSG_HIP(hipMalloc((void**)&counts, ntiles * sizeof(uint32_t)));
-  PSG_HIP(hipMalloc((void**)&miss, m * sizeof(uint64_t)));
+  PSG_HIP(hipMalloc((void**)&counts, (ntiles + 1) * sizeof(uint32_t)));
   k_tile_missing<<<(unsigned)ntiles, kBlock, 0, st>>>(s->slots, n, counts);
   k_scan_counts<<<1, kBlock, 0, st>>>(counts, ntiles);
+  uint32_t m32 = 0;
+  PSG_HIP(hipMemcpyAsync(&m32, counts + ntiles, sizeof(m32), hipMemcpyDeviceToHost, st));
+  PSG_HIP(hipStreamSynchronize(st));
+  const uint64_t m = m32;
+  if (m == 0) {
+    PSG_HIP(hipFree(counts));
+    return PSG_OK;
+  }
+  PSG_HIP(hipMalloc((void**)&miss, m * sizeof(uint64_t)));
   k_compact_missing<<<(unsigned)ntiles, kBlock, 0, st>>>(q, s->slots, n, counts, miss);
   PSG_HIP(hipGetLastError());
   int rc;
@@ -481,16 +621,66 @@ static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, uint64_t 
 // skipped; a pull of an absent key reads 0, which is what its insertion
 // gives) -> read the flags.  Only when keys were absent: insert them (merge),
 // resolve again into slots2, and apply the request to exactly those keys.
+template <int DT, int OP>
+static void launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals,
+                                 void* out, hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  const int vec = ((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out));
+  k_resolve_apply<DT, OP><<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size,
+                                                                s->wlo,
+                                                                s->key_begin,
+                                                                s->key_end, (T*)s->vals, (const T*)vals,
+                                                                (T*)out, s->flags, vec);
+}
+
+template <int DT>
+static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals,
+                         void* out, hipStream_t st) {
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  reset_flags(s);
+  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
+  switch (op) {
+    case PSG_PUSH: launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, st); break;
+    case PSG_PULL: launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, st); break;
+    default: launch_resolve_apply<DT, PSG_PUSH | PSG_PULL>(s, q, n, vals, out, st); break;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+// PSG_SORTED_FUSED=0: the two-pass form (resolve to slots, then k_slots), for A/B runs.
+static bool sorted_fused() {
+  static const bool on = [] {
+    const char* e = getenv("PSG_SORTED_FUSED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static int sorted_request(psg_store* s, int op, const uint64_t* q, const void* vals, void* out,
                           uint64_t n, hipStream_t st) {
   PSG_TRY(ensure_slots(s, n));
-  PSG_TRY(launch_resolve(s, q, n, s->slots, st));
-  PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
+  if (sorted_fused() && s->size > 0) {
+    switch (s->dtype) {
+      case PSG_F32: PSG_TRY(resolve_apply<PSG_F32>(s, op, q, n, vals, out, st)); break;
+      case PSG_F64: PSG_TRY(resolve_apply<PSG_F64>(s, op, q, n, vals, out, st)); break;
+      case PSG_F16: PSG_TRY(resolve_apply<PSG_F16>(s, op, q, n, vals, out, st)); break;
+      default: PSG_TRY(resolve_apply<PSG_BF16>(s, op, q, n, vals, out, st)); break;
+    }
+  } else {
+    PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+    PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
+  }
   PSG_TRY(read_flags(s, st));
   PSG_TRY(check_request_flags(s));
-  const int missing = s->flags_host[F_MISSING];
-  if (missing == 0) return PSG_OK;
-  PSG_TRY(insert_missing(s, q, n, (uint64_t)missing, st));
+  if (s->flags_host[F_MISSING] == 0) return PSG_OK;
+  if (sorted_fused() && s->size > 0) {
+    // the fused pass kept no slots: resolve again (the keys have not changed)
+    // so the insert and the fixup know which keys were absent
+    PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+  }
+  PSG_TRY(insert_missing(s, q, n, st));
   PSG_TRY(launch_resolve(s, q, n, s->slots2, st));
   switch (s->dtype) {
     case PSG_F32: PSG_TRY(run_fixup<PSG_F32>(s, op, vals, out, n, st)); break;
@@ -509,9 +699,8 @@ static int sorted_resolve(psg_store* s, const uint64_t* q, uint64_t n, bool inse
   PSG_TRY(launch_resolve(s, q, n, s->slots, st));
   PSG_TRY(read_flags(s, st));
   PSG_TRY(check_request_flags(s));
-  const int missing = s->flags_host[F_MISSING];
-  if (missing == 0 || !insert) return PSG_OK;
-  PSG_TRY(insert_missing(s, q, n, (uint64_t)missing, st));
+  if (s->flags_host[F_MISSING] == 0 || !insert) return PSG_OK;
+  PSG_TRY(insert_missing(s, q, n, st));
   PSG_TRY(launch_resolve(s, q, n, s->slots, st));
   PSG_TRY(read_flags(s, st));
   PSG_REQUIRE(s->flags_host[F_MISSING] == 0, PSG_ERR_HIP, "SORTED store: keys still absent after insert");
@@ -572,10 +761,12 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
     return rc;
   };
   hipError_t e;
-  if ((e = hipMalloc(&s->flags, F_NFLAGS * sizeof(int))) != hipSuccess)
-    return fail(hip_fail(e, "hipMalloc(flags)", __FILE__, __LINE__));
-  if ((e = hipHostMalloc(&s->flags_host, F_NFLAGS * sizeof(int), hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc(&s->flags_host, F_NFLAGS * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) !=
+      hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc(flags)", __FILE__, __LINE__));
+  if ((e = hipHostGetDevicePointer((void**)&s->flags, s->flags_host, 0)) != hipSuccess)
+    return fail(hip_fail(e, "hipHostGetDevicePointer(flags)", __FILE__, __LINE__));
+  memset(s->flags_host, 0, F_NFLAGS * sizeof(int));
   if (kind == PSG_STORE_DENSE) {
     s->capacity = capacity;
     s->size = capacity;
@@ -606,7 +797,6 @@ int psg_store_destroy(psg_store* s) {
   if (s->slots) (void)hipFree(s->slots);
   if (s->slots2) (void)hipFree(s->slots2);
   if (s->wlo) (void)hipFree(s->wlo);
-  if (s->flags) (void)hipFree(s->flags);
   if (s->flags_host) (void)hipHostFree(s->flags_host);
   delete s;
   return PSG_OK;
@@ -653,7 +843,7 @@ int psg_store_handle(psg_store* s, int flags, const uint64_t* keys, uint64_t fir
       char* base = (char*)s->vals + (first_key - s->key_begin) * s->esize;
       return dense_request(s->dtype, flags, base, vals, out, n, st);
     }
-    PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+    reset_flags(s);
     int rc;
     switch (s->dtype) {
       case PSG_F32: rc = run_dense_keyed<PSG_F32>(s, flags, keys, vals, out, n, st); break;
@@ -681,7 +871,7 @@ int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert
   PSG_REQUIRE(keys, PSG_ERR_INVALID, "psg_store_resolve: null keys");
   hipStream_t st = (hipStream_t)stream;
   if (s->kind == PSG_STORE_DENSE) {
-    PSG_HIP(hipMemsetAsync(s->flags, 0, F_NFLAGS * sizeof(int), st));
+    reset_flags(s);
     k_dense_slots<<<grid_n(n, kBlock), kBlock, 0, st>>>(keys, n, s->key_begin, s->capacity, slots,
                                                          s->flags);
     PSG_HIP(hipGetLastError());
