@@ -191,3 +191,14 @@ def test_reference_local_py_launches_our_binaries(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         assert "Check failed" not in r.stderr and "aborted" not in r.stderr, r.stderr[-2000:]
         assert r.stdout.count(" ok") == expect, r.stdout
+
+
+def test_process_job_ends_when_a_node_dies():
+    """A worker process that dies without a goodbye (std::_Exit after the start
+    barrier): the others see the dropped connection, abort their waits and the
+    job ends non-zero within seconds instead of hanging in Finalize."""
+    exe = os.path.join(BIN, "crash_node")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 2, "-procs", timeout=60)
+    assert r.returncode != 0
+    assert "disconnected" in r.stderr
