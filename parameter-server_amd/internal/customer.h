@@ -8,6 +8,7 @@
 // Customer.cpp:58-67, which KVWorker::OnReceive relies on).
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -22,6 +23,24 @@ namespace ps {
 
 class PostOffice;
 
+/* Spin up to PS_SPIN_US microseconds (default 50) for `ready` before the
+ * caller blocks on its condition variable: a request's round trip crosses
+ * three thread hand-offs (worker -> server queue, server -> worker queue,
+ * worker receive thread -> waiting caller) and a futex wake-up costs more
+ * than the GPU work of a small request. */
+int SpinMicros();
+template <typename Pred>
+bool SpinFor(Pred ready) {
+  const int us = SpinMicros();
+  if (us <= 0) return ready();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0;; ++i) {
+    if (ready()) return true;
+    if ((i & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us)) return false;
+    __builtin_ia32_pause();
+  }
+}
+
 class ThreadsafePQueue {
  public:
   void Push(Message msg) {
@@ -29,14 +48,17 @@ class ThreadsafePQueue {
       std::lock_guard<std::mutex> lk(mu_);
       msg.meta.seq = next_seq_++;
       queue_.push(std::move(msg));
+      size_.store(queue_.size(), std::memory_order_release);
     }
     cv_.notify_one();
   }
   Message WaitAndPop() {
+    SpinFor([this] { return size_.load(std::memory_order_acquire) > 0; });
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [this] { return !queue_.empty(); });
     Message m = queue_.top();
     queue_.pop();
+    size_.store(queue_.size(), std::memory_order_release);
     return m;
   }
 
@@ -49,6 +71,7 @@ class ThreadsafePQueue {
   };
   std::mutex mu_;
   std::condition_variable cv_;
+  std::atomic<size_t> size_{0};
   uint64_t next_seq_ = 0;
   std::priority_queue<Message, std::vector<Message>, Cmp> queue_;
 };
@@ -88,6 +111,7 @@ class Customer {
   std::vector<std::pair<int, int>> tracker_;
   std::condition_variable tracker_cond_;
   std::mutex tracker_mu_;
+  std::atomic<uint64_t> completions_{0};  // requests completed so far (spin target)
 };
 
 }  // namespace ps

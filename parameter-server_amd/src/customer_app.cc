@@ -1,5 +1,7 @@
 // customer_app.cc — Customer (reference src/internal/Customer.cpp:9-70) and
 // SimpleApp (src/ps/SimpleApp.cpp).
+#include <cstdlib>
+
 #include "internal/PostOffice.h"
 #include "internal/customer.h"
 #include "ps/simple_app.h"
@@ -28,7 +30,34 @@ int Customer::NewRequest(int receiver) {
   return (int)tracker_.size() - 1;
 }
 
+int SpinMicros() {
+  static const int us = [] {
+    const char* e = std::getenv("PS_SPIN_US");
+    return e ? std::atoi(e) : 50;
+  }();
+  return us;
+}
+
 void Customer::WaitRequest(int request_id) {
+  {
+    // spin while no request completes; re-check under the lock when one does
+    uint64_t seen = completions_.load(std::memory_order_acquire);
+    bool done;
+    {
+      std::lock_guard<std::mutex> lk(tracker_mu_);
+      done = tracker_[request_id].first == tracker_[request_id].second;
+    }
+    if (done) return;
+    SpinFor([&] {
+      const uint64_t c = completions_.load(std::memory_order_acquire);
+      if (c == seen) return false;
+      seen = c;
+      std::lock_guard<std::mutex> lk(tracker_mu_);
+      done = tracker_[request_id].first == tracker_[request_id].second;
+      return done;
+    });
+    if (done) return;
+  }
   std::unique_lock<std::mutex> lk(tracker_mu_);
   while (tracker_[request_id].first != tracker_[request_id].second) {
     tracker_cond_.wait_for(lk, std::chrono::milliseconds(100));
@@ -47,7 +76,10 @@ int Customer::GetResponse(int request_id) {
 void Customer::AddResponse(int request_id, int cnt) {
   std::lock_guard<std::mutex> lk(tracker_mu_);
   tracker_[request_id].second += cnt;
-  if (tracker_[request_id].first == tracker_[request_id].second) tracker_cond_.notify_all();
+  if (tracker_[request_id].first == tracker_[request_id].second) {
+    completions_.fetch_add(1, std::memory_order_release);
+    tracker_cond_.notify_all();
+  }
 }
 
 void Customer::ReceiveThread() {
@@ -66,7 +98,10 @@ void Customer::ReceiveThread() {
     if (!msg.meta.request) {
       std::lock_guard<std::mutex> lk(tracker_mu_);
       int r = msg.meta.timestamp;
-      if (++tracker_[r].second == tracker_[r].first) tracker_cond_.notify_all();
+      if (++tracker_[r].second == tracker_[r].first) {
+        completions_.fetch_add(1, std::memory_order_release);
+        tracker_cond_.notify_all();
+      }
     }
   }
 }
