@@ -120,7 +120,7 @@ void Barrier(PostOffice* po, int customer_id, int group);
 void NoteStarted(PostOffice* po, int customer_id);
 std::string GroupBroadcast(PostOffice* po, int group, const std::string& mine);
 void Deliver(const Message& msg);
-/* hand msg to the right customer of node dst (Van.cpp:226-237) */
+/* hand msg to the right customer of node dst (Van.cpp:246-257) */
 void DeliverTo(PostOffice* dst, const Message& msg);
 /* wake every waiter with an error after a node failed */
 void Abort(const std::string& why);

@@ -1,0 +1,40 @@
+// internal/shm_pool.h — host frames between processes as shared-memory mappings.
+//
+// In process mode (src/tcp_van.cc) a large host array (>= 1 MiB: the key /
+// value frames of a Push, the values of a Pull reply) is allocated from POSIX
+// shared-memory blocks instead of the heap.  A frame that lies in such a block
+// is sent to a peer on the same host as (block name, offset) and the peer maps
+// the block (once, cached): the frame crosses no socket and no copy, the way
+// HBM frames travel as hipIpc mappings.  On a node with a GPU every block is
+// also registered with HIP (psg_host_register), so the server's H2D staging and
+// the D2H of a reply run at DMA rate from it.
+//
+// Names are "/psg.<pid>.<n>".  The owner unlinks its names when its Van stops
+// (and at exit); the -procs launcher removes what a crashed node left.  A block
+// that /dev/shm cannot hold is not created (posix_fallocate): the array then
+// comes from the heap and travels on the socket.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+namespace ps {
+namespace shm {
+
+/* switch the pool on for this process (process mode; PS_SHM_FRAMES=0 keeps it off) */
+void Enable();
+bool Enabled();
+/* a pooled shared-memory block of >= bytes, or nullptr (pool off / small / no room) */
+std::shared_ptr<void> Alloc(size_t bytes);
+/* this process's block holding [p, p + n): its name and p's offset in it */
+bool Find(const void* p, size_t n, std::string* name, uint64_t* offset);
+/* map a peer's block (cached for the process lifetime); nullptr on failure */
+char* Map(const std::string& name, size_t* size);
+/* remove this process's block names (mappings stay valid) */
+void UnlinkAll();
+/* remove the names a process left behind (the launcher, after a crash) */
+void UnlinkOf(int pid);
+
+}  // namespace shm
+}  // namespace ps

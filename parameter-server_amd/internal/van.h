@@ -32,7 +32,7 @@ class Van {
   int GetAvailableTimestamp() { return timestamp_++; }
 
   /* Process mode (one node per process, src/tcp_van.cc): the barrier runs
-   * through the scheduler (Van.cpp:186-216) and returns true; the local Van
+   * through the scheduler (Van.cpp:187-220) and returns true; the local Van
    * returns false and the in-process cluster barrier is used. */
   virtual bool Barrier(int customer_id, int group) {
     (void)customer_id;

@@ -157,8 +157,8 @@ class SVector {
     std::shared_ptr<T> np;
     if (auto pinned = device::HostAlloc(n * sizeof(T)))  // large frames: pinned, PCIe-rate copies
       np = std::shared_ptr<T>(pinned, static_cast<T*>(pinned.get()));
-    else
-      np = std::shared_ptr<T>(new T[n](), [](T* p) { delete[] p; });
+    else  // left uninitialised: resize() fills what it adds, copies overwrite
+      np = std::shared_ptr<T>(new T[n], [](T* p) { delete[] p; });
     if (size_) std::memcpy(np.get(), data(), size_ * sizeof(T));
     ptr_ = np;
     capacity_ = n;

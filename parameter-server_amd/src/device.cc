@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "internal/PostOffice.h"
+#include "internal/shm_pool.h"
 #include "ps/log.h"
 #include "ps/svector.h"
 
@@ -108,6 +109,11 @@ std::shared_ptr<void> Alloc(size_t bytes, int dev) {
 // staging.  Pooled like the HBM blocks (device key -1).  Off without a GPU
 // or with PS_PINNED_HOST=0.
 std::shared_ptr<void> HostAlloc(size_t bytes) {
+  // process mode: large host arrays live in shared memory, so a frame to a
+  // peer process is a mapping (internal/shm_pool.h)
+  if (shm::Enabled()) {
+    if (auto p = shm::Alloc(bytes)) return p;
+  }
   static const bool enabled = [] {
     const char* e = std::getenv("PS_PINNED_HOST");
     return Count() > 0 && !(e && std::atoi(e) == 0);

@@ -2,11 +2,11 @@
 // runs the reference (local.py:87-114: argv = {prog, config.json, log, role}),
 // a TCP Van between the processes, and a launcher that does local.py's job.
 //
-// Control plane (the reference's Van.cpp:181-442, re-designed for one host):
+// Control plane (the reference's Van.cpp:182-443, re-designed for one host):
 //   * every server / worker binds a listening socket and sends ADD_NODE to the
 //     scheduler at PS_SCHEDULER_URI:PS_SCHEDULER_PORT;
 //   * once PS_NUM_SERVER + PS_NUM_WORKER nodes registered, the scheduler orders
-//     them as Van.cpp:292-296 does (hostname descending, port ascending), gives
+//     them as Van.cpp:333-336 does (hostname descending, port ascending), gives
 //     server / worker ranks in that order and sends every node the table;
 //   * BARRIER requests go to the scheduler, which releases a group once all its
 //     members arrived (for customer c > 0: the members on which customer c
@@ -37,6 +37,8 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -47,6 +49,7 @@
 #include "internal/Env.h"
 #include "internal/PostOffice.h"
 #include "internal/device.h"
+#include "internal/shm_pool.h"
 
 extern char** environ;
 
@@ -214,7 +217,15 @@ struct WireHeader {
 // kPeerFrame: a slice of an HBM frame the RECEIVER sent earlier and this node
 // mapped (a reply that echoes the request's keys, KVApp.h:449-455): sent back
 // as (token, offset) and resolved to the receiver's own array.
-enum FrameKind : uint8_t { kHostFrame = 0, kIpcFrame = 1, kPeerFrame = 2 };
+// kShmFrame: a host frame in one of the sender's shared-memory blocks
+// (internal/shm_pool.h), sent as (block name, offset) and mapped in place.
+enum FrameKind : uint8_t { kHostFrame = 0, kIpcFrame = 1, kPeerFrame = 2, kShmFrame = 3 };
+
+struct ShmFrame {
+  char name[48];
+  uint64_t offset;
+  uint64_t token;
+};
 
 struct PeerFrame {
   uint64_t token;
@@ -304,6 +315,7 @@ class TcpVan : public Van {
   std::shared_ptr<Conn> Connect(int id);
   int Encode(const Message& msg, const Node& to, std::string* head, std::vector<SVector<char>>* host_frames);
   SVector<char> MapFrame(int sender, const IpcFrame& f, uint64_t bytes);
+  SVector<char> MapShmFrame(int sender, const ShmFrame& f, uint64_t bytes);
   void SendControl(int to, Control::Command cmd, int group = 0, int customer_id = 0, const std::string& body = "");
   bool Abandoned() const { return cluster::Aborted(); }
 
@@ -345,6 +357,7 @@ class TcpVan : public Van {
   std::shared_ptr<FrameRegistry> rel_;
   std::atomic<bool> abort_sent_{false};
   bool started_van_ = false;
+  std::atomic<uint64_t> sent_kind_[4] = {};  // frames sent per FrameKind (PS_VAN_STATS=1 prints them)
 };
 
 // ---------------------------------------------------------------------------
@@ -411,7 +424,7 @@ void TcpVan::Start(int customer_id) {
       joined = joined_;
     }
     CHECK(!Abandoned()) << "job aborted during registration: " << cluster::AbortReason();
-    // ranks in address order (Van.cpp:292-296)
+    // ranks in address order (Van.cpp:333-336)
     std::sort(joined.begin(), joined.end(), [](const Node& a, const Node& b) {
       int c = a.hostname.compare(b.hostname);
       return c != 0 ? c > 0 : a.port < b.port;
@@ -472,7 +485,7 @@ void TcpVan::OnAddNode(const Message& msg) {
     reg_cv_.notify_all();
     return;
   }
-  // the node table (Van.cpp:404-431)
+  // the node table (Van.cpp:420-443)
   int my_rank = -1;
   {
     std::lock_guard<std::mutex> lk(peers_mu_);
@@ -690,10 +703,12 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
   PutMeta(meta, msg.meta);
   Writer frames;
   int bytes = 0;
-  const bool can_map = to.gpu && to.hostname == my_node_.hostname;
+  const bool same_host = to.hostname == my_node_.hostname;
+  const bool can_map = to.gpu && same_host;
   for (const SVector<char>& f : msg.data) {
     PeerFrame pf;
-    if (f.on_device() && f.size() && rel_->Find(f.data(), f.size(), to.id, &pf)) {
+    if (f.size() && rel_->Find(f.data(), f.size(), to.id, &pf)) {
+      ++sent_kind_[kPeerFrame];
       frames.pod<uint8_t>(kPeerFrame);
       frames.pod<uint64_t>(f.size());
       frames.pod(pf);
@@ -710,6 +725,7 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
           d.token = next_token_++;
           inflight_[d.token] = f;
         }
+        ++sent_kind_[kIpcFrame];
         frames.pod<uint8_t>(kIpcFrame);
         frames.pod<uint64_t>(f.size());
         frames.pod(d);
@@ -718,11 +734,30 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
       }
       LOG(WARNING) << "hipIpc export of an HBM frame failed (" << psg_last_error() << "); sending its bytes";
     }
+    ShmFrame sf;
+    std::string sname;
+    if (!f.on_device() && f.size() && same_host && shm::Find(f.data(), f.size(), &sname, &sf.offset) &&
+        sname.size() < sizeof(sf.name)) {
+      std::memset(sf.name, 0, sizeof(sf.name));
+      std::memcpy(sf.name, sname.data(), sname.size());
+      {
+        std::lock_guard<std::mutex> lk(frames_mu_);
+        sf.token = next_token_++;
+        inflight_[sf.token] = f;
+      }
+      ++sent_kind_[kShmFrame];
+      frames.pod<uint8_t>(kShmFrame);
+      frames.pod<uint64_t>(f.size());
+      frames.pod(sf);
+      bytes += (int)sizeof(sf);
+      continue;
+    }
     SVector<char> h = f;
     if (f.on_device() && f.size()) {
       h = SVector<char>::Uninitialized(f.size());
       device::CopySync(h.data(), f.data(), f.size(), 1);
     }
+    if (h.size()) ++sent_kind_[kHostFrame];
     frames.pod<uint8_t>(kHostFrame);
     frames.pod<uint64_t>(h.size());
     host_frames->push_back(h);
@@ -785,6 +820,18 @@ SVector<char> TcpVan::MapFrame(int sender, const IpcFrame& f, uint64_t bytes) {
   return SVector<char>(view, bytes, [reg, sender, token](char* p) { reg->Release(p, sender, token); }, f.device);
 }
 
+SVector<char> TcpVan::MapShmFrame(int sender, const ShmFrame& f, uint64_t bytes) {
+  size_t size = 0;
+  char* base = shm::Map(std::string(f.name, strnlen(f.name, sizeof(f.name))), &size);
+  CHECK(base) << "cannot map the shared-memory frame " << f.name << " of node " << sender;
+  CHECK_LE(f.offset + bytes, size) << "shared-memory frame outside its block";
+  std::shared_ptr<FrameRegistry> reg = rel_;
+  const uint64_t token = f.token;
+  char* view = base + f.offset;
+  reg->Add(view, bytes, sender, token);  // a reply may echo it back
+  return SVector<char>(view, bytes, [reg, sender, token](char* p) { reg->Release(p, sender, token); });
+}
+
 void TcpVan::ReadLoop(int fd) {
   int peer = Node::kEmpty;
   bool said_goodbye = false;
@@ -807,6 +854,7 @@ void TcpVan::ReadLoop(int fd) {
         uint64_t bytes;
         IpcFrame ipc;
         PeerFrame peer;
+        ShmFrame shm;
       };
       std::vector<Pending> descs(wh.nframes);
       bool ok = true;
@@ -814,6 +862,7 @@ void TcpVan::ReadLoop(int fd) {
         ok = ok && ReadAll(fd, &d.kind, 1) && ReadAll(fd, &d.bytes, 8);
         if (ok && d.kind == kIpcFrame) ok = ReadAll(fd, &d.ipc, sizeof(d.ipc));
         if (ok && d.kind == kPeerFrame) ok = ReadAll(fd, &d.peer, sizeof(d.peer));
+        if (ok && d.kind == kShmFrame) ok = ReadAll(fd, &d.shm, sizeof(d.shm));
       }
       if (!ok) break;
       for (auto& d : descs) {
@@ -833,6 +882,8 @@ void TcpVan::ReadLoop(int fd) {
             own = it->second;
           }
           msg.data.push_back(own.Slice(d.peer.offset, d.peer.offset + d.bytes));
+        } else if (d.kind == kShmFrame) {
+          msg.data.push_back(MapShmFrame(peer, d.shm, d.bytes));
         } else {
           msg.data.push_back(MapFrame(peer, d.ipc, d.bytes));
         }
@@ -919,6 +970,11 @@ void TcpVan::ReleaseLoop() {
 void TcpVan::Stop() {
   if (!started_van_ || stopping_.exchange(true)) return;
   ready_ = false;
+  if (const char* e = std::getenv("PS_VAN_STATS"); e && std::atoi(e) != 0)
+    std::fprintf(stderr, "van stats node %d: frames sent host=%llu hbm-ipc=%llu echoed=%llu shm=%llu\n",
+                 my_node_.id, (unsigned long long)sent_kind_[kHostFrame].load(),
+                 (unsigned long long)sent_kind_[kIpcFrame].load(), (unsigned long long)sent_kind_[kPeerFrame].load(),
+                 (unsigned long long)sent_kind_[kShmFrame].load());
   {
     std::lock_guard<std::mutex> lk(rel_->mu);
     rel_->closed = true;
@@ -958,8 +1014,11 @@ void TcpVan::Stop() {
     for (int fd : reader_fds_) ::close(fd);
     reader_fds_.clear();
   }
-  std::lock_guard<std::mutex> lk(frames_mu_);
-  inflight_.clear();
+  {
+    std::lock_guard<std::mutex> lk(frames_mu_);
+    inflight_.clear();
+  }
+  shm::UnlinkAll();  // peers have mapped what they use; names go, mappings stay
 }
 
 // ---------------------------------------------------------------------------
@@ -995,6 +1054,7 @@ int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** a
   const char* role = RoleOf(argc, argv);
   CHECK(role) << "process mode needs a role (argv[3] or PS_ROLE)";
   ReadLocalConfigToEnv(argv[1]);
+  shm::Enable();
   const int ns = Environment::GetIntOrDefault("PS_NUM_SERVER", 1);
   const int nw = Environment::GetIntOrDefault("PS_NUM_WORKER", 1);
   const Node::Role r = ParseRole(role);
@@ -1088,6 +1148,7 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(5));
   }
+  for (pid_t q : pids) shm::UnlinkOf((int)q);  // what a crashed node left in /dev/shm
   for (const char* r : {"scheduler", "server", "worker"}) std::remove((dir + "/config_" + r + ".json").c_str());
   if (!std::getenv("PS_KEEP_LOGS")) {
     for (auto& l : logs) std::remove(l.c_str());

@@ -4,6 +4,7 @@
 // GPU.  Built and run by tests/test_host_runtime.py; every check is a CHECK,
 // so a wrong result exits non-zero.
 #include <atomic>
+#include <cstdlib>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -68,7 +69,9 @@ int main(int argc, char* argv[]) {
   if (IsWorker()) {
     KVWorker<float> kv(0, 0);
     const int rank = MyRank(), nw = NumWorkers();
-    const int num = 20000;
+    // keys per request: argv[4] when given (large requests exercise the
+    // shared-memory frames of process mode), else 20000
+    const int num = argc > 4 ? std::atoi(argv[4]) : 20000;
     // disjoint keys per worker (test_kv_app.cpp layout)
     std::vector<Key> keys(num);
     std::vector<float> vals(num);

@@ -202,3 +202,22 @@ def test_process_job_ends_when_a_node_dies():
     r = run(exe, "-ns", 2, "-nw", 2, "-procs", timeout=60)
     assert r.returncode != 0
     assert "disconnected" in r.stderr
+
+
+def test_process_mode_host_frames_travel_as_shared_memory():
+    """Host frames >= 1 MiB between processes on one host are shared-memory
+    mappings (internal/shm_pool.h), not socket bytes; replies that echo the
+    request keys point back into the worker's own frames; /dev/shm is clean
+    afterwards."""
+    import re
+    exe = os.path.join(BIN, "kv_cluster_host")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 2, "-procs", 300000, env={"PS_VAN_STATS": "1"}, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count(" ok") == 2
+    stats = {int(m.group(1)): (int(m.group(2)), int(m.group(3)))
+             for m in re.finditer(r"van stats node (\d+): frames sent host=\d+ hbm-ipc=\d+ echoed=(\d+) shm=(\d+)",
+                                  r.stderr)}
+    assert stats[9][1] > 0 and stats[11][1] > 0, stats  # workers' Push frames
+    assert stats[8][0] > 0 and stats[10][0] > 0, stats  # servers echo the keys back
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("psg.")]
