@@ -1,6 +1,8 @@
 // device.cc — GPU plumbing of the host runtime, all through the psg C-ABI.
 #include "internal/device.h"
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -140,6 +142,16 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
     std::lock_guard<std::mutex> lk(pl.mu);
     pl.free[{-1, rb}].push_back(q);
   });
+}
+
+std::shared_ptr<void> HugeAlloc(size_t bytes) {
+  constexpr size_t kHuge = size_t(2) << 20;
+  if (bytes < 2 * kHuge) return nullptr;
+  const size_t rb = (bytes + kHuge - 1) & ~(kHuge - 1);
+  void* p = std::aligned_alloc(kHuge, rb);
+  if (!p) return nullptr;
+  (void)madvise(p, rb, MADV_HUGEPAGE);
+  return std::shared_ptr<void>(p, [](void* q) { std::free(q); });
 }
 
 void EnableAllPeerAccess() {
