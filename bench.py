@@ -482,15 +482,19 @@ def backend_check_after_probe(backend) -> bool:
 
 def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
     achieved = alg_bytes / (ms * 1e-3) / 1e9
+    # HBM bytes per launch from the committed PMC summaries (tools/pmc_summary.py):
+    # the one measured on this kernel at these algorithmic bytes, if any
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_push_traffic.json")
-    if os.path.exists(pmc) and vb == 4:
+    import glob
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
             d = json.load(open(pmc))
-            if d.get("keys") * 12 == alg_bytes:
-                traffic = d.get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            continue
+        names = [k.split("<")[0].strip() for k in str(d.get("kernel", "")).split("|")]
+        if d.get("alg_bytes_per_launch") == alg_bytes and names and all(n in kernel for n in names):
+            traffic = d.get("hbm_bytes_per_launch")
+            break
     return {
         "kernel": kernel,
         "bound": "hbm",

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes.
 
-usage: pmc_summary.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEYS OUT_JSON
+usage: pmc_summary.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEYS OUT_JSON [ALG_BYTES_PER_KEY]
+
+KERNEL_SUBSTR may name several kernels separated by '|' (the launches of one
+request): their per-launch medians are added.  ALG_BYTES_PER_KEY defaults to
+12 (the dense Push).
 
 FETCH_DIR / WRITE_DIR are the -d output directories of
   rocprofv3 --pmc FETCH_SIZE --output-format csv ...
@@ -36,25 +40,31 @@ def read_counter(d, kernel_sub, counter):
 
 
 def main():
-    fdir, wdir, ksub, keys, out = sys.argv[1:6]
-    fetch = read_counter(fdir, ksub, "FETCH_SIZE")
-    write = read_counter(wdir, ksub, "WRITE_SIZE")
-    if not fetch or not write:
-        print("no counter rows found", len(fetch), len(write))
-        sys.exit(1)
-    f = statistics.median(fetch)
-    w = statistics.median(write)
+    fdir, wdir, ksubs, keys, out = sys.argv[1:6]
+    per_key = int(sys.argv[6]) if len(sys.argv) > 6 else 12
+    f = w = 0.0
+    launches = []
+    for ksub in ksubs.split("|"):
+        fetch = read_counter(fdir, ksub, "FETCH_SIZE")
+        write = read_counter(wdir, ksub, "WRITE_SIZE")
+        if not fetch or not write:
+            print("no counter rows found for", ksub, len(fetch), len(write))
+            sys.exit(1)
+        f += statistics.median(fetch)
+        w += statistics.median(write)
+        launches.append([len(fetch), len(write)])
     hbm = (2 * f + w) * 1024
+    alg = per_key * int(keys)
     res = {
-        "kernel": ksub,
+        "kernel": ksubs,
         "keys": int(keys),
         "fetch_size_kib_median": f,
         "write_size_kib_median": w,
-        "launches": [len(fetch), len(write)],
+        "launches": launches,
         "correction": "gfx950: FETCH_SIZE x2 (wide streaming reads), WRITE_SIZE x1; KiB -> bytes",
         "hbm_bytes_per_launch": int(hbm),
-        "alg_bytes_per_launch": 12 * int(keys),
-        "traffic_over_alg": hbm / (12 * int(keys)),
+        "alg_bytes_per_launch": alg,
+        "traffic_over_alg": hbm / alg,
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
