@@ -53,6 +53,7 @@ struct Pool {
   std::mutex mu;
   std::map<std::pair<int, size_t>, std::vector<void*>> free;
   std::map<size_t, uint64_t> seen;  // pinned-host requests per size class
+  std::map<size_t, bool> pinning;   // a block of this class is being pinned
   static size_t Round(size_t b) {
     if (b <= (64u << 20)) return (b + 65535) & ~size_t(65535);
     size_t r = size_t(64) << 20;
@@ -126,17 +127,29 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
   void* p = nullptr;
   {
     std::lock_guard<std::mutex> lk(pool.mu);
-    // pinning costs far more than one copy: the first request of a size class
-    // stays pageable (a one-shot Push, test_kv_app_benchmark's repeat = 1);
-    // from the second on (a training loop) the block is pinned and pooled
-    if (pool.seen[rb]++ == 0) return nullptr;
     auto& fl = pool.free[{-1, rb}];
     if (!fl.empty()) {
       p = fl.back();
       fl.pop_back();
+    } else {
+      // pinning costs far more than one copy and must not stall a request: a
+      // size class seen before gets a block pinned in the background, which
+      // the next request of that size picks up (a training loop); this one
+      // stays pageable (a one-shot Push, test_kv_app_benchmark's repeat = 1)
+      if (pool.seen[rb]++ > 0 && !pool.pinning[rb]) {
+        pool.pinning[rb] = true;
+        std::thread([rb] {
+          void* q = nullptr;
+          const bool ok = psg_host_alloc(&q, rb) == PSG_OK;
+          Pool& pl = GlobalPool();
+          std::lock_guard<std::mutex> lk2(pl.mu);
+          if (ok) pl.free[{-1, rb}].push_back(q);
+          pl.pinning[rb] = false;
+        }).detach();
+      }
+      return nullptr;
     }
   }
-  if (!p && psg_host_alloc(&p, rb) != PSG_OK) return nullptr;  // fall back to pageable memory
   return std::shared_ptr<void>(p, [rb](void* q) {
     Pool& pl = GlobalPool();
     std::lock_guard<std::mutex> lk(pl.mu);
