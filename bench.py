@@ -538,7 +538,7 @@ def main(argv=None) -> None:
     ap.add_argument("--check", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-keys", type=int, default=10_000_000)
-    ap.add_argument("--cpu-reps", type=int, default=12)
+    ap.add_argument("--cpu-reps", type=int, default=25)
     args = ap.parse_args(argv)
     dtype, _, default_keys, _ = WORKLOADS[args.workload]
     if args.keys is None:
