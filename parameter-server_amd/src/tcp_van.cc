@@ -702,7 +702,7 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
   Writer meta;
   PutMeta(meta, msg.meta);
   Writer frames;
-  int bytes = 0;
+  int64_t bytes = 0;  // frames may exceed 2 GiB (a 1 B-element f16 Push)
   const bool same_host = to.hostname == my_node_.hostname;
   const bool can_map = to.gpu && same_host;
   for (const SVector<char>& f : msg.data) {
@@ -712,7 +712,7 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
       frames.pod<uint8_t>(kPeerFrame);
       frames.pod<uint64_t>(f.size());
       frames.pod(pf);
-      bytes += (int)sizeof(pf);
+      bytes += (int64_t)sizeof(pf);
       continue;
     }
     if (f.on_device() && f.size() && can_map) {
@@ -729,7 +729,7 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
         frames.pod<uint8_t>(kIpcFrame);
         frames.pod<uint64_t>(f.size());
         frames.pod(d);
-        bytes += (int)sizeof(d);
+        bytes += (int64_t)sizeof(d);
         continue;
       }
       LOG(WARNING) << "hipIpc export of an HBM frame failed (" << psg_last_error() << "); sending its bytes";
@@ -749,7 +749,7 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
       frames.pod<uint8_t>(kShmFrame);
       frames.pod<uint64_t>(f.size());
       frames.pod(sf);
-      bytes += (int)sizeof(sf);
+      bytes += (int64_t)sizeof(sf);
       continue;
     }
     SVector<char> h = f;
@@ -761,13 +761,14 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
     frames.pod<uint8_t>(kHostFrame);
     frames.pod<uint64_t>(h.size());
     host_frames->push_back(h);
-    bytes += (int)h.size();
+    bytes += (int64_t)h.size();
   }
   WireHeader wh{kMagic, (uint32_t)meta.b.size(), (uint32_t)msg.data.size(), 0};
   head->assign(reinterpret_cast<const char*>(&wh), sizeof(wh));
   head->append(meta.b);
   head->append(frames.b);
-  return bytes + (int)head->size();
+  bytes += (int64_t)head->size();
+  return bytes > INT32_MAX ? INT32_MAX : (int)bytes;  // Van::SendMsg reports an int
 }
 
 int TcpVan::SendMsg(const Message& msg) {
