@@ -358,29 +358,30 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
 
     for _ in range(args.warmup):
         one_step()
-    marks = [(backend.new_event(), backend.new_event(), backend.new_event())
-             for _ in range(args.steps)]
+    # one HIP event between consecutive phases: e[2k] | Push k | e[2k+1] | Pull k | e[2k+2]
+    # (the end of step k is the start of step k+1: two markers per step, not three)
+    evs = [backend.new_event() for _ in range(2 * args.steps + 1)]
     backend.sync()
     barrier()
     backend.sync()
     t0 = time.perf_counter()
-    for a, b, c in marks:
-        backend.record(a)
+    backend.record(evs[0])
+    for k in range(args.steps):
         if fused:
             backend.step()
-            backend.record(b)
+            backend.record(evs[2 * k + 1])
         else:
             backend.push()
-            backend.record(b)
+            backend.record(evs[2 * k + 1])
             backend.pull()
-        backend.record(c)
+        backend.record(evs[2 * k + 2])
     backend.sync()
     barrier()
     t1 = time.perf_counter()
     local_ms = (t1 - t0) * 1e3 / max(args.steps, 1)
-    n_marks = max(len(marks), 1)
-    push_ms = sum(backend.elapsed(a, b) for a, b, _ in marks) / n_marks
-    pull_ms = sum(backend.elapsed(b, c) for _, b, c in marks) / n_marks
+    n_marks = max(args.steps, 1)
+    push_ms = sum(backend.elapsed(evs[2 * k], evs[2 * k + 1]) for k in range(args.steps)) / n_marks
+    pull_ms = sum(backend.elapsed(evs[2 * k + 1], evs[2 * k + 2]) for k in range(args.steps)) / n_marks
     ms = local_ms
     acc_ms = backend.accumulate_probe() if (world > 1 and hasattr(backend, "accumulate_probe")) else None
     if dist is not None:
