@@ -145,14 +145,18 @@ char* Map(const std::string& name, size_t* size) {
   void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (p == MAP_FAILED) return nullptr;
-  Register(p, n);
-  std::lock_guard<std::mutex> lk(s.mu);
-  auto ins = s.mapped.emplace(name, std::make_pair((char*)p, n));
-  if (!ins.second) {  // mapped by a racing reader meanwhile: keep one
-    munmap(p, n);
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    auto ins = s.mapped.emplace(name, std::make_pair((char*)p, n));
+    if (!ins.second) {  // mapped by a racing reader meanwhile: keep one
+      munmap(p, n);
+      *size = ins.first->second.second;
+      return ins.first->second.first;
+    }
   }
-  *size = ins.first->second.second;
-  return ins.first->second.first;
+  Register(p, n);
+  *size = n;
+  return (char*)p;
 }
 
 void UnlinkAll() {
