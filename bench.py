@@ -171,11 +171,12 @@ class GpuBackend:
             self.node_barrier.wait()
             return
         if self.keyed:
-            kp = self._key_pos()
+            # one server: the slice is the whole request (KVWorker's DefaultSlicer
+            # skips the kernel for a single range; the store's range check covers it)
             if self.comm is None:
                 self.store.handle(self.p.PUSH, self.keys, self.vals, None, self.L, stream=self.stream)
             else:
-                self.comm.push_keyed(self.store, self.keys, self.vals, self.L, kp, self.stream)
+                self.comm.push_keyed(self.store, self.keys, self.vals, self.L, self._key_pos(), self.stream)
         elif self.comm is None:
             self.store.handle(self.p.PUSH, None, self.vals, None, self.L, first_key=0,
                               stream=self.stream)
@@ -189,11 +190,10 @@ class GpuBackend:
             self.node_barrier.wait()
             return
         if self.keyed:
-            kp = self._key_pos()
             if self.comm is None:
                 self.store.handle(self.p.PULL, self.keys, None, self.out, self.L, stream=self.stream)
             else:
-                self.comm.pull_keyed(self.store, self.keys, self.out, self.L, kp, self.stream)
+                self.comm.pull_keyed(self.store, self.keys, self.out, self.L, self._key_pos(), self.stream)
         elif self.comm is None:
             self.store.handle(self.p.PULL, None, None, self.out, self.L, first_key=0,
                               stream=self.stream)
@@ -457,7 +457,7 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
     if world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
                                    "SORTED-store Push: k_tile_windows + k_resolve_apply "
-                                   "(one host sync)", vb)
+                                   "(one host sync; one server, so no slicer pass)", vb)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
                                    "k_dense_vec<PUSH> (store += vals)", vb)

@@ -400,7 +400,14 @@ void KVWorker<Value>::DefaultSlicer(Data& send, const std::vector<Range>& ranges
   sliced->resize(n);
   std::vector<uint64_t> pos(n + 1, 0), vpos(n + 1, 0);
   const size_t nkeys = send.keys.size();
-  if (send.keys.on_device()) {
+  if (send.keys.on_device() && n == 1 && send.lens.empty()) {
+    // one server owns [0, kMaxKey): the slice is the whole request, no kernel
+    // and no host sync.  The one key the reference's slicer would reject
+    // (kMaxKey itself, KVApp.h:544) is rejected by the server's range check.
+    CHECK_EQ(nkeys ? send.vals.size() / nkeys * nkeys : send.vals.size(), send.vals.size());
+    pos[1] = nkeys;
+    vpos[1] = send.vals.size();
+  } else if (send.keys.on_device()) {
     if (send.lens.size()) {
       CHECK_EQ(send.keys.size(), send.lens.size());
       CHECK(send.lens.on_device()) << "device keys need device lens";
