@@ -434,7 +434,7 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
             "workload": (f"{WORKLOADS.get(wl, ('', 0, 0, 'configs[1]'))[3]}: "
                          + (("keyed (10 M sorted uint64 keys, SORTED store), " if wl == "keyed" else "dense, ")
                             + ("1 server + 1 worker, Push then Pull" if world == 1 else
-                               f"ns=nw={world}, BSP Push/Pull over RCCL"))),
+                               f"ns=nw={world}, BSP Push/Pull (see exchange)"))),
             "keys_per_worker": L,
             "shard_keys": blk,
             "parallelism": f"ps{world}",

@@ -7,6 +7,7 @@ per process from PSG_DENSE_UNROLL / PSG_DENSE_NT / PSG_DENSE_BPC).
 usage: sweep_dense.py KEYS [UNROLLS] [NTS] [BPCS] [OP]     e.g. 67108864 1,2,4 1,2,3 2,4,8
 OP = "all" (default: the knobs apply to Push and Pull) or "pull" (the Pull alone,
 PSG_DENSE_PULL_*; the Push keeps its defaults).
+SWEEP_ARGS (env) adds bench.py arguments, e.g. "--workload dense-f16".
 Writes a table to stdout and gpurun_out/sweep_dense_<KEYS>.json.
 """
 import itertools
@@ -32,7 +33,7 @@ rows = []
 for unroll, nt, bpc in itertools.product(unrolls, nts, bpcs):
     env = dict(os.environ, **{pre + "UNROLL": str(unroll), pre + "NT": str(nt), pre + "BPC": str(bpc)})
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--check", "0",
-           "--steps", "30", "--warmup", "3", "--keys", str(keys)]
+           "--steps", "30", "--warmup", "3", "--keys", str(keys)] + os.environ.get("SWEEP_ARGS", "").split()
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
     if r.returncode != 0:
         print("FAILED", unroll, nt, bpc, r.stderr[-400:], flush=True)
