@@ -63,6 +63,7 @@ inline int dtype_size(int dtype) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // Per-dtype arithmetic on one 16-B vector.  Sub-32-bit types accumulate in
 // f32 and round once (RNE): with p(f32)=24 >= 2*p(f16)+2 the double rounding

@@ -49,6 +49,9 @@ __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__
   return lo;
 }
 
+// spare elements after a store's keys: k_resolve_apply's 16-B LDS loads may
+// read 8 B past the last key
+constexpr uint64_t kKeyPad = 2;
 constexpr int kWin = 2048;  // LDS-staged window of store keys (16 KiB: 10 blocks per CU)
 
 // lower_bound by one wave: 64 lanes probe 64 evenly spaced keys per round and
@@ -213,52 +216,44 @@ __global__ __launch_bounds__(256) void k_resolve_apply(const uint64_t* __restric
     if (hi < lo) hi = lo;  // unsorted input
     const uint64_t W = hi - lo;
     const bool staged = W <= (uint64_t)kWin;
-    if (staged)
-      for (uint64_t j = threadIdx.x; j < W; j += kBlock) sK[j] = K[lo + j];
-    __syncthreads();
     const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
-    uint64_t prev = i0 > 0 && i0 < t1 ? q[i0 - 1] : 0;
-    uint32_t r = 0;
-    uint64_t slot[kPerLane];
-    bool hit[kPerLane];
-#pragma unroll
-    for (int k = 0; k < kPerLane; ++k) {
-      const uint64_t i = i0 + k;
-      hit[k] = false;
-      slot[k] = 0;
-      if (i >= t1) continue;
-      const uint64_t key = q[i];
-      if (key < kb || key >= ke) range = 1;
-      if (i > 0 && prev >= key) unsorted = 1;
-      prev = key;
-      uint64_t p;
-      bool found;
-      if (staged) {
-        const uint32_t w = (uint32_t)W;
-        if (k == 0) {
-          r = lower_bound_lds(sK, w, key);
-        } else if (!(r < w && sK[r] >= key)) {
-          if (r + 1 < w && sK[r + 1] >= key) r = r + 1;
-          else r = (r + 1 >= w) ? w : r + 1 + lower_bound_lds(sK + r + 1, w - r - 1, key);
-        }
-        p = lo + r;
-        found = r < w && sK[r] == key;
-      } else {
-        p = lower_bound_dev(K, lo, hi, key);
-        found = p < S && K[p] == key;
-      }
-      hit[k] = found;
-      slot[k] = p;
-      if (!found) missing++;
-    }
-    // apply: the 4 request values / replies of a lane are one 16-B vector
-    // when T is 4 B, the tile is whole and the caller's arrays are 16-B
-    // aligned (vec, checked on the host)
-    T v[kPerLane], o[kPerLane];
     const bool whole = i0 + kPerLane <= t1;
+    // Issue every global load that does not depend on the window before the
+    // barrier — the window's store keys, this lane's request keys, the key
+    // before them and (Push) its values — so a tile costs two dependent HBM
+    // round trips (these, then the store values) instead of one per staging
+    // step plus two.
+    if (staged) {
+      // straight to LDS (no VGPRs): each wave instruction moves 1 KiB of the
+      // window; lanes past its end re-read its start (written, never read).
+      // A lane may read 8 B past K[S-1]: the key arrays carry kKeyPad spare
+      // elements for it.
+      const uint32_t nbytes = (uint32_t)W * 8u;
+      const char* src = reinterpret_cast<const char*>(K + lo);
+      for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += (kBlock / 64) * 1024u) {
+        const uint32_t off = c + (threadIdx.x & 63) * 16u;
+        const char* g = off < nbytes ? src + off : src;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)((char*)sK + c), 16, 0, 0);
+      }
+    }
+    uint64_t key[kPerLane];
+    if (whole && (vec & 2)) {
+      const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0);
+      const u64x2 b = *reinterpret_cast<const u64x2*>(q + i0 + 2);
+      key[0] = a[0];
+      key[1] = a[1];
+      key[2] = b[0];
+      key[3] = b[1];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : 0;
+    }
+    uint64_t prev = i0 > 0 && i0 < t1 ? q[i0 - 1] : 0;
+    T v[kPerLane];
     if constexpr ((OP & PSG_PUSH) != 0) {
       if constexpr (sizeof(T) == 4) {
-        if (whole && vec) {
+        if (whole && (vec & 1)) {
           const f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(vals + i0));
 #pragma unroll
           for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
@@ -271,22 +266,80 @@ __global__ __launch_bounds__(256) void k_resolve_apply(const uint64_t* __restric
         for (int k = 0; k < kPerLane; ++k) v[k] = (i0 + k < t1) ? vals[i0 + k] : (T)0.0f;
       }
     }
+    __syncthreads();
+    uint32_t r = 0;
+    uint64_t slot[kPerLane];
+    bool hit[kPerLane];
 #pragma unroll
     for (int k = 0; k < kPerLane; ++k) {
-      T x = (T)0.0f;
-      if (hit[k]) {
-        x = V[slot[k]];
-        if constexpr ((OP & PSG_PUSH) != 0) {
-          x = E::add1(x, v[k]);
-          V[slot[k]] = x;
+      const uint64_t i = i0 + k;
+      hit[k] = false;
+      slot[k] = 0;
+      if (i >= t1) continue;
+      const uint64_t kk = key[k];
+      if (kk < kb || kk >= ke) range = 1;
+      if (i > 0 && prev >= kk) unsorted = 1;
+      prev = kk;
+      uint64_t p;
+      bool found;
+      if (staged) {
+        const uint32_t w = (uint32_t)W;
+        if (k == 0) {
+          r = lower_bound_lds(sK, w, kk);
+        } else if (!(r < w && sK[r] >= kk)) {
+          if (r + 1 < w && sK[r + 1] >= kk) r = r + 1;
+          else r = (r + 1 >= w) ? w : r + 1 + lower_bound_lds(sK + r + 1, w - r - 1, kk);
         }
+        p = lo + r;
+        found = r < w && sK[r] == kk;
+      } else {
+        p = lower_bound_dev(K, lo, hi, kk);
+        found = p < S && K[p] == kk;
       }
-      o[k] = x;
+      hit[k] = found;
+      slot[k] = p;
+      if (!found) missing++;
+    }
+    // apply.  A lane whose 4 keys are 4 consecutive, 16-B aligned store
+    // slots (the common case: a request that covers a stretch of the store)
+    // moves its store values as one vector; request values and replies are one
+    // vector when T is 4 B, the tile is whole and the caller's arrays are 16-B
+    // aligned (vec & 1, checked on the host)
+    T o[kPerLane];
+    bool done_v = false;
+    if constexpr (sizeof(T) == 4) {
+      if (hit[0] && hit[1] && hit[2] && hit[3] && slot[3] == slot[0] + 3 && (slot[0] & 3) == 0) {
+        const f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + slot[0]));
+        T y[kPerLane];
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) {
+          y[k] = x[k];
+          if constexpr ((OP & PSG_PUSH) != 0) y[k] = E::add1(y[k], v[k]);
+          o[k] = y[k];
+        }
+        if constexpr ((OP & PSG_PUSH) != 0)
+          *reinterpret_cast<u32x4*>(V + slot[0]) = __builtin_bit_cast(u32x4, f32x4{y[0], y[1], y[2], y[3]});
+        done_v = true;
+      }
+    }
+    if (!done_v) {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        T x = (T)0.0f;
+        if (hit[k]) {
+          x = V[slot[k]];
+          if constexpr ((OP & PSG_PUSH) != 0) {
+            x = E::add1(x, v[k]);
+            V[slot[k]] = x;
+          }
+        }
+        o[k] = x;
+      }
     }
     if constexpr ((OP & PSG_PULL) != 0) {
       bool done = false;
       if constexpr (sizeof(T) == 4) {
-        if (whole && vec) {
+        if (whole && (vec & 1)) {
           *reinterpret_cast<u32x4*>(outv + i0) = __builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]});
           done = true;
         }
@@ -569,7 +622,7 @@ static int merge_insert(psg_store* s, const uint64_t* miss, uint64_t m, hipStrea
   PSG_REQUIRE(cap <= 0xfffffffeull, PSG_ERR_RANGE, "SORTED store: more than 2^32-2 keys");
   uint64_t* K2 = nullptr;
   T* V2 = nullptr;
-  PSG_HIP(hipMalloc((void**)&K2, cap * sizeof(uint64_t)));
+  PSG_HIP(hipMalloc((void**)&K2, (cap + kKeyPad) * sizeof(uint64_t)));
   PSG_HIP(hipMalloc((void**)&V2, cap * sizeof(T)));
   if (S) k_merge_old<T><<<grid_n(S, kBlock), kBlock, 0, st>>>(s->keys, (const T*)s->vals, S, miss, m, K2, V2);
   k_merge_new<T><<<grid_n(m, kBlock), kBlock, 0, st>>>(s->keys, S, miss, m, K2, V2);
@@ -626,7 +679,9 @@ static void launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, co
                                  void* out, hipStream_t st) {
   using T = typename Elem<DT>::T;
   const uint64_t ntiles = (n + kTile - 1) / kTile;
-  const int vec = ((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out));
+  // bit 0: request values / replies 16-B aligned; bit 1: request keys 16-B aligned
+  const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
+                  (aligned16(q) ? 2 : 0);
   k_resolve_apply<DT, OP><<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size,
                                                                 s->wlo,
                                                                 s->key_begin,
@@ -781,7 +836,7 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
       PSG_REQUIRE(capacity <= 0xfffffffeull, PSG_ERR_RANGE, "SORTED store capacity above 2^32-2");
       if ((e = hipMalloc(&s->vals, capacity * es)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(store values)", __FILE__, __LINE__));
-      if ((e = hipMalloc(&s->keys, capacity * sizeof(uint64_t))) != hipSuccess)
+      if ((e = hipMalloc(&s->keys, (capacity + kKeyPad) * sizeof(uint64_t))) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(store keys)", __FILE__, __LINE__));
       s->capacity = capacity;
     }
