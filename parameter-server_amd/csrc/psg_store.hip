@@ -80,12 +80,12 @@ __device__ __forceinline__ uint64_t lower_bound_wave(const uint64_t* __restrict_
 // tile: wlo[t] = lower_bound(K, q[t * kTile]); wlo[ntiles] = lower_bound(K, q[n-1]) + 1.
 __global__ __launch_bounds__(256) void k_tile_windows(const uint64_t* __restrict__ q, uint64_t n,
                                                       const uint64_t* __restrict__ K, uint64_t S,
-                                                      uint64_t* __restrict__ wlo) {
-  const uint64_t ntiles = (n + kTile - 1) / kTile;
+                                                      uint64_t* __restrict__ wlo, uint64_t tile) {
+  const uint64_t ntiles = (n + tile - 1) / tile;
   const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
   for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t <= ntiles; t += waves) {
     if (t < ntiles) {
-      const uint64_t r = lower_bound_wave(K, S, q[t * kTile]);
+      const uint64_t r = lower_bound_wave(K, S, q[t * tile]);
       if ((threadIdx.x & 63) == 0) wlo[t] = r;
     } else {
       const uint64_t h = lower_bound_wave(K, S, q[n - 1]);
@@ -193,8 +193,8 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 // instead of 36: request key 8 + store key 8 + value 4 + store value 8).  An
 // absent key is skipped (a pull reads 0, what its insertion gives); the flags
 // tell the host to insert it and apply the request to it afterwards.
-template <int DT, int OP>
-__global__ __launch_bounds__(256) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
+template <int DT, int OP, int NT>
+__global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
                                                        const uint64_t* __restrict__ K, uint64_t S,
                                                        const uint64_t* __restrict__ wlo, uint64_t kb,
                                                        uint64_t ke,
@@ -204,18 +204,20 @@ __global__ __launch_bounds__(256) void k_resolve_apply(const uint64_t* __restric
                                                        int* __restrict__ flags, int vec) {
   using E = Elem<DT>;
   using T = typename E::T;
-  __shared__ uint64_t sK[kWin];
+  constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
+  constexpr uint32_t winN = 2 * NT * kPerLane;          // LDS window of store keys
+  __shared__ uint64_t sK[winN];
   int missing = 0, range = 0, unsorted = 0;
-  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  const uint64_t ntiles = (n + tileN - 1) / tileN;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t t0 = tile * kTile;
-    const uint64_t t1 = (t0 + kTile < n) ? t0 + kTile : n;
+    const uint64_t t0 = tile * tileN;
+    const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
     const uint64_t lo = wlo[tile];
     uint64_t hi = tile + 1 < ntiles ? wlo[tile + 1] + 1 : wlo[ntiles];
     if (hi > S) hi = S;
     if (hi < lo) hi = lo;  // unsorted input
     const uint64_t W = hi - lo;
-    const bool staged = W <= (uint64_t)kWin;
+    const bool staged = W <= (uint64_t)winN;
     const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
     const bool whole = i0 + kPerLane <= t1;
     // Issue every global load that does not depend on the window before the
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(256) void k_resolve_apply(const uint64_t* __restric
       // elements for it.
       const uint32_t nbytes = (uint32_t)W * 8u;
       const char* src = reinterpret_cast<const char*>(K + lo);
-      for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += (kBlock / 64) * 1024u) {
+      for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += (NT / 64) * 1024u) {
         const uint32_t off = c + (threadIdx.x & 63) * 16u;
         const char* g = off < nbytes ? src + off : src;
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
@@ -547,7 +549,7 @@ static int launch_resolve(psg_store* s, const uint64_t* q, uint64_t n, uint32_t*
                           hipStream_t st) {
   const uint64_t ntiles = (n + kTile - 1) / kTile;
   reset_flags(s);
-  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
+  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, kTile);
   k_resolve<<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
                                                   s->key_end, slots, s->flags);
   PSG_HIP(hipGetLastError());
@@ -674,27 +676,49 @@ static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, hipStream
 // skipped; a pull of an absent key reads 0, which is what its insertion
 // gives) -> read the flags.  Only when keys were absent: insert them (merge),
 // resolve again into slots2, and apply the request to exactly those keys.
+// Block size of the fused kernel (PSG_RA_BLOCK = 256 | 512 | 1024, default
+// 1024).  The tile is 4 keys per lane, so a larger block leaves fewer windows
+// to search (10 M keys: k_tile_windows 11.2 -> 8.8 us from 256 to 512; keyed
+// Push+Pull 606 / 660 / 675 GB/s at 256 / 512 / 1024).
+static int ra_block() {
+  static const int nt = [] {
+    const char* e = getenv("PSG_RA_BLOCK");
+    const int v = e ? atoi(e) : 0;
+    return v == 256 || v == 512 ? v : 1024;
+  }();
+  return nt;
+}
+
 template <int DT, int OP>
 static void launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals,
                                  void* out, hipStream_t st) {
   using T = typename Elem<DT>::T;
-  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  const int nt = ra_block();
+  const uint64_t ntiles = (n + (uint64_t)nt * kPerLane - 1) / ((uint64_t)nt * kPerLane);
   // bit 0: request values / replies 16-B aligned; bit 1: request keys 16-B aligned
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
                   (aligned16(q) ? 2 : 0);
-  k_resolve_apply<DT, OP><<<grid_n(ntiles, 1), kBlock, 0, st>>>(q, n, s->keys, s->size,
-                                                                s->wlo,
-                                                                s->key_begin,
-                                                                s->key_end, (T*)s->vals, (const T*)vals,
-                                                                (T*)out, s->flags, vec);
+  if (nt == 1024)
+    k_resolve_apply<DT, OP, 1024><<<grid_n(ntiles, 1), 1024, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
+                                                                     s->key_end, (T*)s->vals, (const T*)vals,
+                                                                     (T*)out, s->flags, vec);
+  else if (nt == 512)
+    k_resolve_apply<DT, OP, 512><<<grid_n(ntiles, 1), 512, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
+                                                                   s->key_end, (T*)s->vals, (const T*)vals,
+                                                                   (T*)out, s->flags, vec);
+  else
+    k_resolve_apply<DT, OP, 256><<<grid_n(ntiles, 1), 256, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
+                                                                   s->key_end, (T*)s->vals, (const T*)vals,
+                                                                   (T*)out, s->flags, vec);
 }
 
 template <int DT>
 static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals,
                          void* out, hipStream_t st) {
-  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  const uint64_t tile = (uint64_t)ra_block() * kPerLane;
+  const uint64_t ntiles = (n + tile - 1) / tile;
   reset_flags(s);
-  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo);
+  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, tile);
   switch (op) {
     case PSG_PUSH: launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, st); break;
     case PSG_PULL: launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, st); break;
