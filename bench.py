@@ -8,15 +8,21 @@ HBM, keys implicit and consecutive):
   N = 1   configs[1]: 1 server + 1 worker, L = 64 M floats.  Push is the
           KVServerDefaultHandle accumulate (src/ps/KVApp.h:446-454) as one
           streaming HIP kernel over the DENSE store; Pull is the read-back.
-  N > 1   configs[2] shape, one process per GPU, rank r = worker r + server
-          shard r (L / N keys): Push = RCCL reduce-scatter + the accumulate
-          kernel, Pull = RCCL all-gather (psg_comm_push / psg_comm_pull), or
-          the two pipelined over buckets (psg_comm_push_pull) — whichever a
-          short calibration in the warm-up finds faster on this node.
+  N > 1   configs[2]: one process per GPU, rank r = worker r + server shard r,
+          L = 256 M floats per worker (L / N keys per shard): Push = RCCL
+          reduce-scatter + the accumulate kernel, Pull = RCCL all-gather
+          (psg_comm_push / psg_comm_pull), the two pipelined over buckets
+          (psg_comm_push_pull), or the one-shot xGMI kernels (psg_xgmi_*) —
+          whichever a short calibration in the warm-up finds faster here.
 
 value = (B * L pushed + B * L pulled) * N / (max-over-ranks time per step),
 B = bytes per value (weak scaling: every worker moves L values each way at
-every N).  `--workload dense-f16` runs configs[4] (f16 values, 1 B per worker).
+every N).  `--workload dense-f16` runs configs[4] (f16 values, 1 G per worker),
+`--workload keyed` configs[3] (10 M sorted uint64 keys, SORTED stores).
+
+The N > 1 job is bootstrapped without torch (psg_group.SocketGroup: a loopback
+star with rank 0 as the rendezvous), so libpsgpu.so runs on /opt/rocm's HIP and
+RCCL at every N; the line names the libraries the process mapped.
 
 Prints ONE JSON line on rank 0.  Launch for N > 1:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -27,6 +33,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -40,25 +47,27 @@ PUSH_ACCESSES = 3      # read vals + read store + write store
 PULL_ACCESSES = 2      # read store + write out
 
 WORKLOADS = {
-    # name: (dtype name, value bytes, default values per worker, description)
-    "dense": ("f32", 4, 64 << 20, "configs[1]"),
-    "dense-f16": ("f16", 2, 1 << 30, "configs[4]"),
-    "keyed": ("f32", 4, 10_000_000, "configs[3]"),
+    # name: (dtype name, value bytes, values per worker at N = 1, at N > 1, configs entry)
+    "dense": ("f32", 4, 64 << 20, 256 << 20, "configs[1]", "configs[2]"),
+    "dense-f16": ("f16", 2, 1 << 30, 1 << 30, "configs[4]", "configs[4]"),
+    "keyed": ("f32", 4, 10_000_000, 10_000_000, "configs[3]", "configs[3]"),
 }
 # algorithmic HBM bytes per key of one keyed Push on the SORTED store:
 # request key 8 + store key 8 (resolve) + value 4 + store value read/write 8
 # (the resolve is fused with the apply: no slot array goes to HBM and back)
 KEYED_PUSH_BYTES = 28
+# pushes outside warmup + steps that a run may make (calibration, verification)
+EXTRA_PUSH_BOUND = 64
 
 
 class GpuBackend:
     """The product path: psg C-ABI (HIP kernels + RCCL)."""
 
-    def __init__(self, rank: int, world: int, local_rank: int, dist=None, dtype="f32",
+    def __init__(self, rank: int, world: int, local_rank: int, group=None, dtype="f32",
                  keyed=False):
         import psg
         self.p = psg
-        self.rank, self.world, self.dist = rank, world, dist
+        self.rank, self.world, self.group = rank, world, group
         self.dt = {"f32": psg.F32, "f16": psg.F16}[dtype]
         self.vb = {"f32": 4, "f16": 2}[dtype]
         self.keyed = keyed
@@ -73,6 +82,7 @@ class GpuBackend:
         self.mode = "rccl"  # "rccl" (RS + AG, or pipelined when fused) or "xgmi"
         self.fused = False
         self.nbuckets = 1
+        self.max_pushes = 1 << 10
 
     def setup(self, L: int, seed: int):
         p = self.p
@@ -93,18 +103,23 @@ class GpuBackend:
         else:
             self.store = p.Store(p.DENSE, self.dt, lo, lo + blk, blk)
         self.vals = p.DeviceBuffer(L * self.vb)
-        # integer-valued 0..7 (f16 holds them and their sums exactly) / 0..999 (f32)
-        self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self._hi(), self.stream)
+        self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self.hi(), self.stream)
         self.out = p.DeviceBuffer(L * self.vb)
         if self.world > 1:
             if not self.share_gpu:
-                uid = [p.comm_id() if self.rank == 0 else None]
-                self.dist.broadcast_object_list(uid, src=0)
-                self.comm = p.Comm(uid[0], self.world, self.rank)
+                uid = self.group.broadcast(p.comm_id() if self.rank == 0 else None)
+                self.comm = p.Comm(uid, self.world, self.rank)
             self.scratch = p.DeviceBuffer(blk * self.vb)
             if not self.keyed:
                 self._setup_xgmi()
         self.sync()
+
+    def hi(self) -> float:
+        """Integer values 0..hi-1, so every partial sum is exact: 0..999 in f32;
+        in f16 small enough that world * pushes * (hi - 1) stays <= 2048."""
+        if self.dt == self.p.F32:
+            return 1000.0
+        return float(max(2, min(8, 2048 // (self.world * self.max_pushes) + 1)))
 
     def _setup_xgmi(self):
         """Map every peer's request vector and shard (hipIpc) for the one-shot
@@ -123,12 +138,10 @@ class GpuBackend:
             print(f"rank {self.rank}: hipIpc export unavailable ({e}); xGMI exchange off",
                   file=sys.stderr)
             mine = None
-        allh = [None] * self.world
-        self.dist.all_gather_object(allh, mine)
+        allh = self.group.all_gather(mine)
         if any(h is None for h in allh):
             return
-        tag = [uuid.uuid4().hex[:16] if self.rank == 0 else None]
-        self.dist.broadcast_object_list(tag, src=0)
+        tag = self.group.broadcast(uuid.uuid4().hex[:16] if self.rank == 0 else None)
         vptrs, sptrs, ok = [], [], True
         try:
             for r in range(self.world):
@@ -141,13 +154,11 @@ class GpuBackend:
                     sptrs.append(p.ipc_open(allh[r][1]))
                     self._peer_ptrs.append(sptrs[-1])
             x = p.Xgmi(self.world, self.rank, vptrs, sptrs)
-            b = p.NodeBarrier("psg_bench_" + tag[0], self.world, self.rank)
+            b = p.NodeBarrier("psg_bench_" + tag, self.world, self.rank)
         except Exception as e:  # noqa: BLE001
             print(f"rank {self.rank}: xGMI mapping failed ({e}); xGMI exchange off", file=sys.stderr)
             ok = False
-        oks = [None] * self.world
-        self.dist.all_gather_object(oks, ok)
-        if not all(oks):
+        if not all(self.group.all_gather(ok)):
             for ptr in self._peer_ptrs:
                 p.ipc_close(ptr)
             self._peer_ptrs = []
@@ -159,9 +170,6 @@ class GpuBackend:
         # the worker's DefaultSlicer on its HBM keys (psg_slice), every request
         kp, _ = self.p.slice_keys(self.keys, self.L, self.begins, self.ends, stream=self.stream)
         return kp
-
-    def _hi(self):
-        return 1000.0 if self.dt == self.p.F32 else 8.0
 
     # -- one phase at a time (N = 1, or the sequential RS / AG at N > 1)
     def push(self):
@@ -209,14 +217,14 @@ class GpuBackend:
         self.mode, self.nbuckets = mode, nb
         self.fused = mode == "rccl" and nb > 1
 
-    def calibrate(self, dist, iters=3):
+    def calibrate(self, iters=3):
         """Pick the exchange for this node by timing each candidate a few times
         (wall clock, barrier-synced): RCCL reduce-scatter then all-gather, the
         RCCL pipelined over 4/8/16 buckets, or the one-shot xGMI kernels.  The
         max over ranks decides, so every rank picks the same."""
+        self.pushes_in_calibration = 0
         if self.world == 1 or self.keyed:
             return
-        import torch
         cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
         if self.xgmi is not None:
             cands.append(("xgmi", 0))
@@ -225,23 +233,22 @@ class GpuBackend:
             self._set_mode(cand)
             self._one_step()
             self.sync()
-            dist.barrier()
+            self.group.barrier()
             t0 = time.perf_counter()
             for _ in range(iters):
                 self._one_step()
             self.sync()
             times.append((time.perf_counter() - t0) * 1e3 / iters)
-            dist.barrier()
-        t = torch.tensor(times, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        order = sorted(range(len(cands)), key=lambda i: t[i].item())
+            self.group.barrier()
+        t = self.group.allreduce_max(times)
+        order = sorted(range(len(cands)), key=lambda i: t[i])
         self._set_mode(cands[order[0]])
         self.calibration = {f"{m}{'' if m == 'xgmi' else '/' + str(nb)}": round(x, 4)
-                            for (m, nb), x in zip(cands, t.tolist())}
+                            for (m, nb), x in zip(cands, t)}
         self.pushes_in_calibration = len(cands) * (iters + 1)
         if self.mode == "xgmi":
             self.pushes_in_calibration += 1
-            self.exchange_verified = self._verify_xgmi(dist)
+            self.exchange_verified = self._verify_xgmi()
             if not self.exchange_verified:
                 rest = [cands[i] for i in order if cands[i][0] != "xgmi"]
                 if not rest:
@@ -251,7 +258,7 @@ class GpuBackend:
                       file=sys.stderr)
                 self._set_mode(rest[0])
 
-    def _verify_xgmi(self, dist) -> bool:
+    def _verify_xgmi(self) -> bool:
         """One xGMI Push + Pull, then every rank's pulled block w must carry the
         same psg_checksum as rank w's own shard (read locally): catches a stale
         or torn cross-GPU read before the timed steps rely on the path."""
@@ -261,11 +268,8 @@ class GpuBackend:
         nb = self.blk * self.vb
         mine = p.checksum(self.store.info().vals, nb, self.stream)
         got = [p.checksum(self.out.ptr + w * nb, nb, self.stream) for w in range(self.world)]
-        owners = [None] * self.world
-        dist.all_gather_object(owners, mine)
-        ok = [None] * self.world
-        dist.all_gather_object(ok, got == owners)
-        return all(ok)
+        owners = self.group.all_gather(mine)
+        return all(self.group.all_gather(got == owners))
 
     def _one_step(self):
         if self.fused:
@@ -289,7 +293,8 @@ class GpuBackend:
 
     def accumulate_probe(self, iters=10):
         """The dominant local kernel at N > 1: the shard accumulate after the
-        reduce-scatter (12 B per f32 element), timed alone with HIP events."""
+        reduce-scatter (12 B per f32 element), timed alone with HIP events.
+        Runs after the parity check: it changes the shards."""
         if self.keyed:
             return None
         a, b = self.new_event(), self.new_event()
@@ -316,38 +321,109 @@ class GpuBackend:
         return ("k_dense_vec<PUSH> on the shard after the reduce-scatter",
                 PUSH_ACCESSES * self.vb * self.blk)
 
-    def check(self, steps_done: int) -> bool:
+    def check(self, steps_done: int) -> dict:
         """After `steps_done` pushes every shard holds steps * sum_w vals_w
-        (integer-valued, exact in f32 and in f16 at the default sizes)."""
+        (integer-valued, exact).  One more Pull, then:
+          device  every element of the pulled vector — every rank's block, i.e.
+                  the peers' shards as they arrived over the exchange — against
+                  the closed form (psg_verify_synth_sum);
+          oracle  a sample at the start of every block w replayed through the
+                  CPU restatement of KVServerDefaultHandle (oracle.Store): each
+                  worker's Push of every step as one request, in worker order."""
         import numpy as np
         import oracle
+        p = self.p
         self.pull()
         self.sync()
-        n = min(self.L, 1 << 20)
-        npt = {self.p.F32: np.float32, self.p.F16: np.float16}[self.dt]
-        got = self.out.download(npt, n, self.stream).astype(np.float64)
-        exp = np.zeros(n)
-        odt = {self.p.F32: oracle.F32, self.p.F16: oracle.F16}[self.dt]
+        bad, first = p.verify_synth_sum(self.out, self.L, self.dt, self._seed, self.world,
+                                        0.0, self.hi(), float(steps_done), stream=self.stream)
+        npt = {p.F32: np.float32, p.F16: np.float16}[self.dt]
+        odt = {p.F32: oracle.F32, p.F16: oracle.F16}[self.dt]
+        m = min(self.blk, 4096)
+        sample_ok = True
         for w in range(self.world):
-            s = oracle.synth(n, odt, self._seed + w, 0, 0.0, self._hi())
-            exp += (s.view(np.float16) if self.dt == self.p.F16 else s).astype(np.float64)
-        return bool(np.array_equal(got, exp * steps_done))
+            lo = w * self.blk
+            got = self.out.download(npt, m, self.stream, offset=lo * self.vb)
+            # element i of worker r's vector is synth(seed + r + i): start the
+            # generator at i = lo instead of producing the whole prefix
+            src = [oracle.synth(m, odt, self._seed + r + lo, 0, 0.0, self.hi()) for r in range(self.world)]
+            st = oracle.Store(odt)
+            for _ in range(steps_done):
+                for r in range(self.world):
+                    st.handle(oracle.PUSH, None, src[r], m, first_key=lo)
+            exp = st.handle(oracle.PULL, None, None, m, first_key=lo)
+            sample_ok &= bool(np.array_equal(got.view(np.uint16) if self.dt == p.F16 else got,
+                                             exp))
+        return {"ok": bad == 0 and sample_ok, "device_mismatches": bad, "first_bad": first,
+                "oracle_sample_ok": sample_ok, "elements": self.L, "oracle_sample": m * self.world}
+
+    def probe_256m(self, n=256 << 20, iters=10):
+        """The north star's own target: one 256 M-float Push (and Pull) on the
+        DENSE store, HIP-event timed on the kernels' stream (N = 1)."""
+        p = self.p
+        st = p.Store(p.DENSE, p.F32, 0, n, n)
+        v, o = p.DeviceBuffer(n * 4), p.DeviceBuffer(n * 4)
+        v.fill_synth(n, p.F32, self._seed, 0, 0.0, 1000.0, self.stream)
+        for _ in range(2):
+            st.handle(p.PUSH, None, v, None, n, stream=self.stream)
+            st.handle(p.PULL, None, None, o, n, stream=self.stream)
+        e = [p.Event() for _ in range(3)]
+        e[0].record(self.stream)
+        for _ in range(iters):
+            st.handle(p.PUSH, None, v, None, n, stream=self.stream)
+        e[1].record(self.stream)
+        for _ in range(iters):
+            st.handle(p.PULL, None, None, o, n, stream=self.stream)
+        e[2].record(self.stream)
+        self.sync()
+        push_ms, pull_ms = e[0].elapsed_ms(e[1]) / iters, e[1].elapsed_ms(e[2]) / iters
+        bad, _ = p.verify_synth_sum(o, n, p.F32, self._seed, 1, 0.0, 1000.0, float(2 + iters),
+                                    stream=self.stream)
+        st.close()
+        v.free()
+        o.free()
+        out = {"keys": n, "push_ms": round(push_ms, 5), "pull_ms": round(pull_ms, 5),
+               "parity_check": bad == 0}
+        for name, ms, acc in (("push", push_ms, PUSH_ACCESSES), ("pull", pull_ms, PULL_ACCESSES)):
+            gbs = acc * 4 * n / (ms * 1e-3) / 1e9
+            out[f"{name}_achieved"] = round(gbs, 1)
+            out[f"{name}_frac"] = round(gbs / HBM_PEAK_GBS, 4)
+        out["kernel"] = "k_dense_vec<PUSH> / <PULL>, 12 / 8 B per float"
+        return out
 
 
-def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
+class _LocalGroup:
+    """World of one (no peers)."""
+    rank, world = 0, 1
+
+    def all_gather(self, obj):
+        return [obj]
+
+    def broadcast(self, obj=None, src=0):
+        return obj
+
+    def barrier(self):
+        pass
+
+    def allreduce_max(self, xs):
+        return list(xs)
+
+    def close(self):
+        pass
+
+
+def run(backend, args, rank: int, world: int, group=None) -> dict | None:
     L = args.keys
     assert L % world == 0, "keys must divide by the number of shards"
+    group = group or _LocalGroup()
     backend._seed = args.seed
+    backend.max_pushes = args.warmup + args.steps + EXTRA_PUSH_BOUND
     backend.setup(L, args.seed)
     extra_pushes = 0
-    if hasattr(backend, "calibrate") and dist is not None:
-        backend.calibrate(dist)
+    if hasattr(backend, "calibrate") and world > 1:
+        backend.calibrate()
         extra_pushes = getattr(backend, "pushes_in_calibration", 0)
     fused = getattr(backend, "fused", False)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
 
     def one_step():
         if fused:
@@ -366,7 +442,7 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
     sampled = [k for k in range(args.steps) if k % every == 0]
     evs = {k: (backend.new_event(), backend.new_event(), backend.new_event()) for k in sampled}
     backend.sync()
-    barrier()
+    group.barrier()
     backend.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -385,31 +461,26 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         if e:
             backend.record(e[2])
     backend.sync()
-    barrier()
+    group.barrier()
     t1 = time.perf_counter()
     local_ms = (t1 - t0) * 1e3 / max(args.steps, 1)
     n_marks = max(len(sampled), 1)
     push_ms = sum(backend.elapsed(a, b) for a, b, _ in evs.values()) / n_marks
     pull_ms = sum(backend.elapsed(b, c) for _, b, c in evs.values()) / n_marks
-    ms = local_ms
-    acc_ms = backend.accumulate_probe() if (world > 1 and hasattr(backend, "accumulate_probe")) else None
-    if dist is not None:
-        import torch
-        t = torch.tensor([local_ms, push_ms, pull_ms, acc_ms or 0.0], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, push_ms, pull_ms, acc = t.tolist()
-        acc_ms = acc if acc_ms is not None else None
-    total_pushes = args.warmup + args.steps + extra_pushes + (10 if acc_ms is not None else 0)
-    ok = None
+    total_pushes = args.warmup + args.steps + extra_pushes
+    chk = None
     if args.check:
-        # the accumulate probe adds the (last reduce-scatter) scratch 10 more times,
-        # which breaks the closed form; only check when no probe ran
-        ok = backend.check(total_pushes) if acc_ms is None else backend_check_after_probe(backend)
-        if dist is not None:
-            import torch
-            f = torch.tensor([0 if ok else 1], dtype=torch.int32)
-            dist.all_reduce(f, op=dist.ReduceOp.MAX)
-            ok = f.item() == 0
+        # the whole pulled vector at every N, before anything else touches the shards
+        chk = backend.check(total_pushes)
+        if not isinstance(chk, dict):
+            chk = {"ok": bool(chk)}
+    acc_ms = backend.accumulate_probe() if (world > 1 and hasattr(backend, "accumulate_probe")) else None
+    ms, push_ms, pull_ms, acc = group.allreduce_max([local_ms, push_ms, pull_ms, acc_ms or 0.0])
+    acc_ms = acc if acc_ms is not None else None
+    ok = None
+    if chk is not None:
+        oks = group.all_gather(bool(chk["ok"]))
+        ok = all(oks)
     if rank != 0:
         return None
     vb = getattr(backend, "vb", 4)
@@ -417,6 +488,8 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
     value_gbs = payload / (ms * 1e-3) / 1e9
     blk = L // world
     wl = getattr(args, "workload", "dense")
+    spec = WORKLOADS.get(wl, WORKLOADS["dense"])
+    cfg = spec[4] if world == 1 else spec[5]
     res = {
         "metric": "device-resident KV Push+Pull GB/s (float vals)",
         "value": round(value_gbs, 3),
@@ -428,10 +501,10 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": WORKLOADS.get(wl, ("f32",))[0],
+        "dtype": spec[0],
         "data": "synthetic (integer-valued floats, seed 7+rank, generated in HBM)",
         "config": {
-            "workload": (f"{WORKLOADS.get(wl, ('', 0, 0, 'configs[1]'))[3]}: "
+            "workload": (f"{cfg}: "
                          + (("keyed (10 M sorted uint64 keys, SORTED store), " if wl == "keyed" else "dense, ")
                             + ("1 server + 1 worker, Push then Pull" if world == 1 else
                                f"ns=nw={world}, BSP Push/Pull (see exchange)"))),
@@ -443,6 +516,12 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         "pull_ms": None if fused else round(pull_ms, 5),
         "parity_check": ok,
     }
+    if chk is not None and world == 1:
+        res["parity_detail"] = {k: v for k, v in chk.items() if k != "ok"}
+    elif chk is not None:
+        res["parity_detail"] = {"checked": "every rank's whole pulled vector on the device "
+                                           "+ an oracle replay at the start of every block",
+                                "elements_per_rank": L}
     if world > 1 and hasattr(backend, "nbuckets"):
         if getattr(backend, "mode", "rccl") == "xgmi":
             res["config"]["exchange"] = "one-shot xGMI kernels (psg_xgmi push/pull, peers via hipIpc)"
@@ -454,6 +533,8 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
         res["config"]["calibration_ms"] = getattr(backend, "calibration", None)
         if hasattr(backend, "exchange_verified"):
             res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
+        if getattr(backend, "share_gpu", False):
+            res["config"]["shared_gpu_test_mode"] = True
     if world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
                                    "SORTED-store Push: k_tile_windows + k_resolve_apply "
@@ -471,23 +552,13 @@ def run(backend, args, rank: int, world: int, dist=None) -> dict | None:
                                    "k_dense_vec<PUSH> on the shard after the reduce-scatter", vb)
     else:
         res["roofline"] = None
+    if (world == 1 and wl == "dense" and hasattr(backend, "probe_256m")
+            and not getattr(args, "no_probe256", False)):
+        res["push256_roofline"] = backend.probe_256m()
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)
+    res["runtime_libs"] = mapped_runtime_libs()
     return res
-
-
-def backend_check_after_probe(backend) -> bool:
-    """With the probe having re-added the scratch, check the Pull equals the shards
-    (all-gather correctness) instead of the closed form."""
-    import numpy as np
-    backend.pull()
-    backend.sync()
-    npt = {backend.p.F32: np.float32, backend.p.F16: np.float16}[backend.dt]
-    got = backend.out.download(npt, backend.L, backend.stream)
-    _, mine = backend.store.dump()
-    mine = mine.view(np.float16) if backend.dt == backend.p.F16 else mine
-    lo = backend.rank * backend.blk
-    return bool(np.array_equal(got[lo:lo + backend.blk], mine[:backend.blk]))
 
 
 def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
@@ -517,24 +588,71 @@ def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
     }
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args) -> dict:
-    """The reference handler (std::unordered_map, one thread) restated in oracle/,
-    on the test_kv_app_benchmark layout: 10 M keys, 1 inserting Push, then
-    `reps` steady Push + Pull.  Reported beside the GPU number, not a target."""
+    """The reference handler (std::unordered_map, one thread — KVServerDefaultHandle,
+    src/ps/KVApp.h:433-458, runs on one Customer thread) restated in oracle/, on the
+    GPU value's own workload: configs[1]'s keys 0..L-1 with the same synthetic
+    values, 1 inserting Push then `reps` steady Push + Pull.  A second, labelled
+    sample times configs[0]'s test_kv_app_benchmark layout (10 M keys at
+    kMaxKey/num*i).  Reported beside the GPU number, not a target."""
     import oracle
     num, reps = args.cpu_keys, args.cpu_reps
     t0 = time.perf_counter()
-    first, push_s, pull_s = oracle.bench(num, reps)
+    first, push_s, pull_s = oracle.bench_layout(num, reps, 0, 1, args.seed)
     wall = time.perf_counter() - t0
-    return {
+    out = {
         "value": round(2 * 4 * num / (push_s + pull_s) / 1e9, 4),
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"{num} keys (kMaxKey/num*i layout), 1 inserting Push ({first:.2f} s) then "
-                   f"{reps} steady Push+Pull through KVServerDefaultHandle's unordered_map loop, "
-                   f"single thread, {wall:.1f} s total"),
+        "config": "configs[1] (the GPU value's workload)",
+        "sample": (f"{num} keys 0..{num - 1} (configs[1] DENSE layout, values seed {args.seed}), "
+                   f"1 inserting Push ({first:.2f} s) then {reps} steady Push+Pull through "
+                   f"KVServerDefaultHandle's unordered_map loop, single thread, {wall:.1f} s total"),
+        "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()},
     }
+    if args.cpu_configs0_keys:
+        n0 = args.cpu_configs0_keys
+        t0 = time.perf_counter()
+        f0, p0, l0 = oracle.bench(n0, 2)
+        out["configs0_sample"] = {
+            "value": round(2 * 4 * n0 / (p0 + l0) / 1e9, 4), "unit": "GB/s",
+            "sample": (f"configs[0] layout: {n0} keys at kMaxKey/num*i "
+                       f"(test_kv_app_benchmark.cpp:47-52), 1 inserting Push ({f0:.2f} s) "
+                       f"then 2 steady Push+Pull, {time.perf_counter() - t0:.1f} s"),
+        }
+    return out
+
+
+def mapped_runtime_libs() -> dict:
+    """Paths of the HIP runtime and RCCL this process mapped (the bench line says
+    which ROCm the numbers come from)."""
+    found = {}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) < 6:
+                    continue
+                path = parts[5]
+                base = os.path.basename(path)
+                for key in ("libamdhip64", "librccl", "libpsgpu"):
+                    if base.startswith(key):
+                        found.setdefault(key, os.path.realpath(path))
+    except OSError:
+        pass
+    return found
 
 
 def main(argv=None) -> None:
@@ -549,29 +667,31 @@ def main(argv=None) -> None:
     ap.add_argument("--event-every", type=int, default=5,
                     help="record the kernel-timing HIP events on every n-th timed step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-keys", type=int, default=10_000_000)
-    ap.add_argument("--cpu-reps", type=int, default=25)
+    ap.add_argument("--no-probe256", action="store_true")
+    ap.add_argument("--cpu-keys", type=int, default=64 << 20)
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-configs0-keys", type=int, default=10_000_000,
+                    help="also time configs[0]'s layout at this many keys (0: skip)")
     args = ap.parse_args(argv)
-    dtype, _, default_keys, _ = WORKLOADS[args.workload]
-    if args.keys is None:
-        args.keys = default_keys
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
-    dist = None
+    dtype, _, keys1, keysn = WORKLOADS[args.workload][:4]
+    if args.keys is None:
+        args.keys = keys1 if world == 1 else keysn
+    group = None
     if world > 1:
-        import torch  # noqa: F401  (load torch's HIP runtime before libpsgpu)
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    backend = GpuBackend(rank, world, local_rank, dist, dtype, keyed=args.workload == "keyed")
-    res = run(backend, args, rank, world, dist)
+        from psg_group import SocketGroup
+        group = SocketGroup(rank, world)
+    backend = GpuBackend(rank, world, local_rank, group, dtype, keyed=args.workload == "keyed")
+    res = run(backend, args, rank, world, group)
     if res is not None:
         print(json.dumps(res), flush=True)
-    if dist is not None:
-        dist.barrier()
+    if group is not None:
+        group.barrier()
     if backend.xgmi is not None:
         backend.sync()
         backend.node_barrier.wait()  # no peer still reads a buffer this rank unmaps
@@ -582,8 +702,8 @@ def main(argv=None) -> None:
     if backend.comm is not None:
         backend.sync()
         backend.comm.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if group is not None:
+        group.close()
 
 
 if __name__ == "__main__":

@@ -134,6 +134,15 @@ int psg_fill_keys_arith(uint64_t* keys, uint64_t n, uint64_t base, uint64_t step
  * xGMI pull against the owners' shards) without moving the data to the host.
  * No reference counterpart: test/verification support. */
 int psg_checksum(const void* dptr, uint64_t nbytes, uint64_t* sum_host, psg_stream stream);
+/* Closed-form check of a pulled vector of integer-valued synthetic pushes:
+ * counts i < n with got[i] != scale * sum_{w < nseeds} synth(seed0 + w, i + offset)
+ * (psg_fill_synth mode 0 over [lo, hi), summed in double).  *first_bad_host
+ * (may be NULL) gets the smallest mismatching index, or UINT64_MAX.
+ * Synchronises `stream`.  No reference counterpart: it checks a whole
+ * multi-GPU Pull — every rank's block — on the device (bench.py, tests). */
+int psg_verify_synth_sum(const void* dptr, uint64_t n, int dtype, uint64_t seed0, int nseeds,
+                         uint64_t offset, double lo, double hi, double scale,
+                         uint64_t* mismatches_host, uint64_t* first_bad_host, psg_stream stream);
 
 /* ======================================================================== */
 /* Server-side value store  (KVServerDefaultHandle::store, KVApp.h:457)      */

@@ -54,6 +54,9 @@ def lib() -> C.CDLL:
         L.oracle_glibc_rand_mod.restype = None
         L.oracle_bench.argtypes = [u64, i32, C.POINTER(f64), C.POINTER(f64), C.POINTER(f64)]
         L.oracle_bench.restype = None
+        L.oracle_bench_layout.argtypes = [u64, i32, u64, u64, u64, C.POINTER(f64),
+                                          C.POINTER(f64), C.POINTER(f64)]
+        L.oracle_bench_layout.restype = None
         _lib = L
     return _lib
 
@@ -152,4 +155,12 @@ def glibc_rand_mod(seed: int, mod: int, n: int):
 def bench(num: int, reps: int):
     a, b, c = C.c_double(), C.c_double(), C.c_double()
     lib().oracle_bench(num, reps, C.byref(a), C.byref(b), C.byref(c))
+    return a.value, b.value, c.value
+
+
+def bench_layout(num: int, reps: int, key_base: int = 0, key_step: int = 1, seed: int = 7):
+    """The handler on the GPU bench's workload (keys base + i*step, synth values)."""
+    a, b, c = C.c_double(), C.c_double(), C.c_double()
+    lib().oracle_bench_layout(num, reps, key_base, key_step, seed, C.byref(a), C.byref(b),
+                              C.byref(c))
     return a.value, b.value, c.value

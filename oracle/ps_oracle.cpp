@@ -367,4 +367,34 @@ void oracle_bench(uint64_t num, int reps, double* first_push_s, double* push_s, 
   *pull_s = reps ? tl / reps : 0;
 }
 
+// CPU baseline on the GPU bench's own workload (configs[1]): keys
+// key_base + i * key_step (step 1: the DENSE layout, keys 0..num-1 of server
+// 0's range) and the bench's integer-valued synthetic values (seed, 0..999).
+// Same handler and timing split as oracle_bench.
+void oracle_bench_layout(uint64_t num, int reps, uint64_t key_base, uint64_t key_step,
+                         uint64_t seed, double* first_push_s, double* push_s, double* pull_s) {
+  std::vector<uint64_t> keys(num);
+  std::vector<float> vals(num), out(num);
+  for (uint64_t i = 0; i < num; ++i) keys[i] = key_base + i * key_step;
+  oracle_synth(vals.data(), num, F32, seed, 0, 0.0, 1000.0);
+  Store<F32> st;
+  using clk = std::chrono::steady_clock;
+  auto t0 = clk::now();
+  handle<F32>(&st, PUSH, keys.data(), 0, vals.data(), nullptr, num);
+  auto t1 = clk::now();
+  *first_push_s = std::chrono::duration<double>(t1 - t0).count();
+  double tp = 0, tl = 0;
+  for (int r = 0; r < reps; ++r) {
+    auto a = clk::now();
+    handle<F32>(&st, PUSH, keys.data(), 0, vals.data(), nullptr, num);
+    auto b = clk::now();
+    handle<F32>(&st, PULL, keys.data(), 0, nullptr, out.data(), num);
+    auto c = clk::now();
+    tp += std::chrono::duration<double>(b - a).count();
+    tl += std::chrono::duration<double>(c - b).count();
+  }
+  *push_s = reps ? tp / reps : 0;
+  *pull_s = reps ? tl / reps : 0;
+}
+
 }  // extern "C"

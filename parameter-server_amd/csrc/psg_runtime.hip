@@ -91,6 +91,54 @@ __global__ __launch_bounds__(256) void k_checksum(const uint64_t* __restrict__ w
   }
 }
 
+// Closed-form check of a pulled vector: got[i] == scale * sum_{w < nseeds} of
+// the integer-valued synth value of (seed0 + w, i + offset), computed in double
+// (exact for the integer sums the bench and tests use).  Per block: mismatch
+// count and the smallest mismatching index (plain stores, the host reduces).
+template <typename T>
+__global__ __launch_bounds__(256) void k_verify_synth_sum(const T* __restrict__ got, uint64_t n,
+                                                          uint64_t seed0, int nseeds, uint64_t offset,
+                                                          double lo, double hi, double scale,
+                                                          uint64_t* __restrict__ part) {
+  const double inv24 = 1.0 / 16777216.0;
+  uint64_t bad = 0, first = ~0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    double e = 0.0;
+    for (int w = 0; w < nseeds; ++w) {
+      const uint64_t r = splitmix64(seed0 + (uint64_t)w + offset + i) >> 40;
+      e += floor((double)r * (hi - lo) * inv24) + lo;
+    }
+    e *= scale;
+    double g;
+    if constexpr (sizeof(T) < 4) g = (double)(float)got[i]; else g = (double)got[i];
+    if (g != e) {
+      bad++;
+      if (i < first) first = i;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    bad += __shfl_xor(bad, o, 64);
+    const uint64_t f = __shfl_xor(first, o, 64);
+    first = f < first ? f : first;
+  }
+  __shared__ uint64_t sb[kBlock / 64], sf[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = bad;
+    sf[threadIdx.x >> 6] = first;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b = 0, f = ~0ull;
+    for (int k = 0; k < kBlock / 64; ++k) {
+      b += sb[k];
+      f = sf[k] < f ? sf[k] : f;
+    }
+    part[2 * blockIdx.x] = b;
+    part[2 * blockIdx.x + 1] = f;
+  }
+}
+
 static unsigned grid_for(uint64_t n) {
   uint64_t b = (n + kBlock - 1) / kBlock;
   uint64_t cap = (uint64_t)max_stream_blocks();
@@ -284,6 +332,54 @@ int psg_checksum(const void* dptr, uint64_t nbytes, uint64_t* sum_host, psg_stre
   uint64_t h = 0;
   for (uint64_t x : host) h += x;
   *sum_host = h;
+  return PSG_OK;
+}
+
+int psg_verify_synth_sum(const void* dptr, uint64_t n, int dtype, uint64_t seed0, int nseeds,
+                         uint64_t offset, double lo, double hi, double scale,
+                         uint64_t* mismatches_host, uint64_t* first_bad_host, psg_stream stream) {
+  PSG_REQUIRE(mismatches_host, PSG_ERR_INVALID, "psg_verify_synth_sum: null out");
+  PSG_REQUIRE(nseeds >= 0, PSG_ERR_INVALID, "psg_verify_synth_sum: nseeds < 0");
+  *mismatches_host = 0;
+  if (first_bad_host) *first_bad_host = UINT64_MAX;
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_verify_synth_sum: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = grid_for(n);
+  uint64_t* part = nullptr;
+  PSG_HIP(hipMalloc((void**)&part, (size_t)g * 2 * sizeof(uint64_t)));
+  switch (dtype) {
+    case PSG_F32:
+      k_verify_synth_sum<float><<<g, kBlock, 0, s>>>((const float*)dptr, n, seed0, nseeds, offset, lo, hi, scale, part);
+      break;
+    case PSG_F64:
+      k_verify_synth_sum<double><<<g, kBlock, 0, s>>>((const double*)dptr, n, seed0, nseeds, offset, lo, hi, scale, part);
+      break;
+    case PSG_F16:
+      k_verify_synth_sum<_Float16><<<g, kBlock, 0, s>>>((const _Float16*)dptr, n, seed0, nseeds, offset, lo, hi, scale, part);
+      break;
+    case PSG_BF16:
+      k_verify_synth_sum<__bf16><<<g, kBlock, 0, s>>>((const __bf16*)dptr, n, seed0, nseeds, offset, lo, hi, scale, part);
+      break;
+    default:
+      (void)hipFree(part);
+      set_error("psg_verify_synth_sum: bad dtype %d", dtype);
+      return PSG_ERR_UNSUPPORTED;
+  }
+  std::vector<uint64_t> host((size_t)g * 2);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(host.data(), part, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(part);
+  if (e != hipSuccess) return hip_fail(e, "psg_verify_synth_sum", __FILE__, __LINE__);
+  uint64_t bad = 0, first = UINT64_MAX;
+  for (unsigned b = 0; b < g; ++b) {
+    bad += host[2 * b];
+    first = host[2 * b + 1] < first ? host[2 * b + 1] : first;
+  }
+  *mismatches_host = bad;
+  if (first_bad_host) *first_bad_host = first;
   return PSG_OK;
 }
 

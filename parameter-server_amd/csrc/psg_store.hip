@@ -268,6 +268,11 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
         for (int k = 0; k < kPerLane; ++k) v[k] = (i0 + k < t1) ? vals[i0 + k] : (T)0.0f;
       }
     }
+    // The window reaches LDS by DMA (global_load_lds), which only vmcnt
+    // tracks; the barrier's workgroup fence does not wait on it in
+    // non-tgsplit mode.  Wait explicitly so no wave reads another wave's part
+    // of the window before it has landed.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     uint32_t r = 0;
     uint64_t slot[kPerLane];

@@ -25,6 +25,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <cstring>
 #include <string>
 
@@ -79,8 +80,10 @@ struct psg_barrier {
   struct Shared {
     std::atomic<int> count;
     std::atomic<int> generation;
-    int nranks;
+    std::atomic<int> broken;  // set by a rank whose wait timed out: every later wait fails
+    std::atomic<int> ready;   // kReady once rank 0 has created the segment
   };
+  static constexpr int kReady = 0x50534742;
   Shared* sh;
   int nranks, rank;
   std::string name;
@@ -198,22 +201,52 @@ int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, ps
 }
 
 // ---- node barrier: a sense-counting barrier in a POSIX shared-memory page --
+// Rank 0 creates the segment exclusively (a name left over by a crashed job is
+// an error, never a stale count); the other ranks wait for it to appear.  A
+// wait that times out has already counted itself in, so it poisons the
+// barrier: every later wait on it, in any rank, fails instead of releasing a
+// phase early.
 int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier** out) {
   PSG_REQUIRE(name && out && nranks > 0 && rank >= 0 && rank < nranks, PSG_ERR_INVALID,
               "psg_node_barrier_create: bad arguments");
   std::string nm = std::string("/") + name;
-  int fd = shm_open(nm.c_str(), O_CREAT | O_RDWR, 0600);
-  PSG_REQUIRE(fd >= 0, PSG_ERR_INVALID, "shm_open(%s) failed", nm.c_str());
-  if (ftruncate(fd, 4096) != 0) {
-    close(fd);
-    set_error("ftruncate(%s) failed", nm.c_str());
-    return PSG_ERR_INVALID;
+  int fd = -1;
+  if (rank == 0) {
+    fd = shm_open(nm.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    PSG_REQUIRE(fd >= 0, PSG_ERR_INVALID, "shm_open(%s, O_EXCL) failed: %s (a stale segment of another job?)",
+                nm.c_str(), strerror(errno));
+    if (ftruncate(fd, 4096) != 0) {
+      close(fd);
+      shm_unlink(nm.c_str());
+      set_error("ftruncate(%s) failed", nm.c_str());
+      return PSG_ERR_INVALID;
+    }
+  } else {
+    for (int tries = 0; (fd = shm_open(nm.c_str(), O_RDWR, 0600)) < 0; ++tries) {
+      PSG_REQUIRE(errno == ENOENT && tries < 60000, PSG_ERR_COMM,
+                  "node barrier %s: rank 0 never created it (%s)", nm.c_str(), strerror(errno));
+      usleep(1000);
+    }
   }
   void* p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   PSG_REQUIRE(p != MAP_FAILED, PSG_ERR_INVALID, "mmap(%s) failed", nm.c_str());
+  auto* sh = (psg_barrier::Shared*)p;  // zero-filled on creation
+  if (rank == 0) {
+    sh->ready.store(psg_barrier::kReady, std::memory_order_release);
+  } else {
+    // rank 0 may not have sized the segment yet: wait for its ready mark
+    for (int tries = 0; sh->ready.load(std::memory_order_acquire) != psg_barrier::kReady; ++tries) {
+      if (tries >= 60000) {
+        munmap(p, 4096);
+        set_error("node barrier %s: never became ready", nm.c_str());
+        return PSG_ERR_COMM;
+      }
+      usleep(1000);
+    }
+  }
   psg_barrier* b = new psg_barrier();
-  b->sh = (psg_barrier::Shared*)p;  // zero-filled on creation: count 0, generation 0
+  b->sh = sh;
   b->nranks = nranks;
   b->rank = rank;
   b->name = nm;
@@ -223,6 +256,8 @@ int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier*
 
 int psg_node_barrier_wait(psg_barrier* b, double timeout_s) {
   PSG_REQUIRE(b, PSG_ERR_INVALID, "psg_node_barrier_wait: null barrier");
+  PSG_REQUIRE(!b->sh->broken.load(std::memory_order_acquire), PSG_ERR_COMM,
+              "node barrier %s is broken (a rank timed out in it)", b->name.c_str());
   const int gen = b->sh->generation.load(std::memory_order_acquire);
   if (b->sh->count.fetch_add(1, std::memory_order_acq_rel) + 1 == b->nranks) {
     b->sh->count.store(0, std::memory_order_relaxed);
@@ -233,9 +268,15 @@ int psg_node_barrier_wait(psg_barrier* b, double timeout_s) {
   clock_gettime(CLOCK_MONOTONIC, &t0);
   for (uint64_t spin = 0; b->sh->generation.load(std::memory_order_acquire) == gen; ++spin) {
     if ((spin & 1023) == 1023) {
+      PSG_REQUIRE(!b->sh->broken.load(std::memory_order_acquire), PSG_ERR_COMM,
+                  "node barrier %s is broken (a rank timed out in it)", b->name.c_str());
       clock_gettime(CLOCK_MONOTONIC, &t);
       const double el = (t.tv_sec - t0.tv_sec) + 1e-9 * (t.tv_nsec - t0.tv_nsec);
-      PSG_REQUIRE(el < timeout_s, PSG_ERR_COMM, "node barrier %s: timed out after %.1f s", b->name.c_str(), el);
+      if (el >= timeout_s) {
+        b->sh->broken.store(1, std::memory_order_release);
+        set_error("node barrier %s: timed out after %.1f s (barrier now broken)", b->name.c_str(), el);
+        return PSG_ERR_COMM;
+      }
       if (el > 1e-3) usleep(20);
     }
   }

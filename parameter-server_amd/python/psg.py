@@ -39,6 +39,7 @@ EXPORTS = [
     "psg_memset", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
     "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
     "psg_event_elapsed_ms", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
+    "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
     "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
@@ -96,6 +97,8 @@ def lib() -> C.CDLL:
             "psg_fill_synth": ([vp, u64, i32, u64, i32, f64, f64, vp], i32),
             "psg_fill_keys_arith": ([vp, u64, u64, u64, vp], i32),
             "psg_checksum": ([vp, u64, C.POINTER(u64), vp], i32),
+            "psg_verify_synth_sum": ([vp, u64, i32, u64, i32, u64, f64, f64, f64,
+                                      C.POINTER(u64), C.POINTER(u64), vp], i32),
             "psg_store_create": ([i32, i32, u64, u64, u64, C.POINTER(vp)], i32),
             "psg_store_destroy": ([vp], i32),
             "psg_store_get_info": ([vp, C.POINTER(StoreInfo)], i32),
@@ -269,6 +272,15 @@ def checksum(ptr, nbytes: int, stream=None) -> int:
     h = C.c_uint64(0)
     _call("psg_checksum", C.c_void_p(_ptr(ptr)), C.c_uint64(nbytes), C.byref(h), _s(stream))
     return h.value
+
+
+def verify_synth_sum(ptr, n: int, dtype: int, seed0: int, nseeds: int, lo: float, hi: float,
+                     scale: float, offset: int = 0, stream=None):
+    """psg_verify_synth_sum: (mismatches, first mismatching index or None)."""
+    bad, first = C.c_uint64(0), C.c_uint64(0)
+    _call("psg_verify_synth_sum", C.c_void_p(_ptr(ptr)), n, dtype, seed0, nseeds, offset, lo, hi,
+          scale, C.byref(bad), C.byref(first), _s(stream))
+    return bad.value, (None if first.value == (1 << 64) - 1 else first.value)
 
 
 def checksum_host(a: np.ndarray) -> int:

@@ -1,0 +1,107 @@
+"""BASELINE.json configs[2..4] at their own sizes on the one MI355X a test box has.
+
+  configs[2]  ns = nw = 8, 256 M floats per worker: bench.py's N > 1 job with 8
+              rank processes sharing the GPU (PSG_BENCH_SHARE_GPU=1 — the one-shot
+              xGMI exchange kernels over hipIpc-mapped peers; RCCL refuses two
+              ranks on one GPU), every rank's WHOLE pulled vector checked.
+  configs[3]  LR-like keyed BSP: 10 M sorted uint64 keys, nw = ns = 4 SORTED
+              shards, through psg_slice (DefaultSlicer, KVApp.h:515-574),
+              psg_store_handle (KVServerDefaultHandle, KVApp.h:433-458) and
+              psg_merge (the pull merge, KVApp.h:680-720), against the oracle
+              doing the same on std::unordered_map.
+  configs[4]  1 G fp16 dense values (one GPU holds a whole 8-shard job's model),
+              Push / Pull with an integer-valued closed form.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+import psg
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    assert psg.device_count() >= 1, "no GPU visible"
+    psg.set_device(0)
+    yield
+
+
+def test_configs2_n8_256m_per_worker_shared_gpu():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PSG_BENCH_SHARE_GPU="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "8", "--keys", str(256 << 20),
+           "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert res["n_gpus"] == 8 and res["config"]["keys_per_worker"] == 256 << 20
+    assert res["config"]["shard_keys"] == 32 << 20
+    assert res["parity_check"] is True, res
+    assert res["config"].get("xgmi_checksum_verified") is True, res
+    # the bench process bootstraps without torch: HIP / RCCL are /opt/rocm's
+    libs = res["runtime_libs"]
+    assert "libamdhip64" in libs and "torch" not in libs["libamdhip64"], libs
+
+
+def test_configs4_f16_1g_dense():
+    import argparse
+    import bench
+    args = argparse.Namespace(keys=1 << 30, seed=7, warmup=1, steps=3, check=1, event_every=1,
+                              no_cpu_baseline=True, no_probe256=True, workload="dense-f16")
+    res = bench.run(bench.GpuBackend(0, 1, 0, None, "f16"), args, 0, 1)
+    assert res["parity_check"] is True, res
+    assert res["parity_detail"]["device_mismatches"] == 0 and res["parity_detail"]["elements"] == 1 << 30
+    assert res["dtype"] == "f16" and res["config"]["workload"].startswith("configs[4]")
+
+
+def test_configs3_keyed_10m_ns4_vs_oracle():
+    n, ns, nw, steps = 10_000_000, 4, 4, 2
+    rng = np.random.default_rng(9)
+    keys = np.unique(rng.integers(0, (1 << 64) - 1, int(n * 1.01) + 1024, dtype=np.uint64))
+    keys = np.sort(rng.choice(keys, n, replace=False))
+    vals = [oracle.synth(n, oracle.F32, 100 + w, 1, -1.0, 1.0) for w in range(nw)]
+    begins, ends = psg.server_ranges(ns)
+    st = psg.Stream()
+    dk = psg.DeviceBuffer.from_numpy(keys)
+    dv = [psg.DeviceBuffer.from_numpy(v) for v in vals]
+    kp, _ = psg.slice_keys(dk, n, begins, ends, stream=st)
+    okp = oracle.slice_keys(keys, *oracle.server_ranges(ns))
+    assert okp is not None and np.array_equal(kp, okp[0])
+    stores = [psg.Store(psg.SORTED, psg.F32, int(begins[s]), int(ends[s]), 0) for s in range(ns)]
+    ostores = [oracle.Store(oracle.F32) for _ in range(ns)]
+    for _ in range(steps):
+        for w in range(nw):  # BSP: every worker's Push of the same key set, in worker order
+            for s in range(ns):
+                a, b = int(kp[s]), int(kp[s + 1])
+                stores[s].handle(psg.PUSH, dk.ptr + 8 * a, dv[w].ptr + 4 * a, None, b - a, stream=st)
+                ostores[s].handle(oracle.PUSH, keys[a:b], vals[w][a:b], b - a)
+    outs, osegs = [], []
+    for s in range(ns):
+        a, b = int(kp[s]), int(kp[s + 1])
+        o = psg.DeviceBuffer(max(b - a, 1) * 4)
+        stores[s].handle(psg.PULL, dk.ptr + 8 * a, None, o, b - a, stream=st)
+        outs.append((o, b - a, int(keys[a])))
+        osegs.append((ostores[s].handle(oracle.PULL, keys[a:b], None, b - a), int(keys[a])))
+    merged = psg.DeviceBuffer(n * 4)
+    psg.merge(list(reversed(outs)), 4, merged, n, stream=st)  # replies in any order
+    got = merged.download(np.float32, n, st)
+    exp = oracle.merge(list(reversed(osegs)), n)
+    assert np.array_equal(got, exp)  # bit-exact: same adds in the same order per key
+    for s in range(ns):
+        k, v = stores[s].dump()
+        ok, ov = ostores[s].dump()
+        order = np.argsort(ok)
+        assert np.array_equal(k, ok[order]) and np.array_equal(v, ov[order])

@@ -92,10 +92,15 @@ def _rank_main(rank, world, port, outdir):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
     import bench
+    from psg_group import SocketGroup
+    # bench.py's own torch-free rendezvous orchestrates; gloo carries only this
+    # backend's data (the collectives RCCL carries on the GPU)
+    group = SocketGroup(rank, world, path=os.path.join(outdir, "rdzv"))
     args = argparse.Namespace(keys=12288, seed=7, warmup=1, steps=3, check=1, no_cpu_baseline=True)
-    res = bench.run(CpuCollectiveBackend(rank, world, dist), args, rank, world, dist)
+    res = bench.run(CpuCollectiveBackend(rank, world, dist), args, rank, world, group)
     with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
         json.dump(res, f)
+    group.close()
     dist.barrier()
     dist.destroy_process_group()
 
@@ -126,3 +131,38 @@ def test_bench_distributed_path_gloo(world):
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in r0
+
+
+def _group_rank(rank, world, port, q):
+    sys.path[:0] = [os.path.join(ROOT, "parameter-server_amd", "python")]
+    os.environ["MASTER_PORT"] = str(port)  # default rendezvous name: parent pid + MASTER_PORT
+    from psg_group import SocketGroup
+    g = SocketGroup(rank, world, timeout_s=60)
+    ag = g.all_gather((rank, b"h" * rank))
+    bc = g.broadcast({"uid": b"\x01\x02"} if rank == 0 else None)
+    mx = g.allreduce_max([float(rank), -float(rank), 7.0])
+    for _ in range(20):
+        g.barrier()
+    g.close()
+    q.put((rank, ag, bc, mx))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_socket_group_collectives(world):
+    """bench.py's torch-free rendezvous (psg_group.SocketGroup): rank-ordered
+    all_gather, broadcast from rank 0, element-wise max, repeated barriers."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, ag, bc, mx in res:
+        assert ag == [(r, b"h" * r) for r in range(world)]
+        assert bc == {"uid": b"\x01\x02"}
+        assert mx == [float(world - 1), 0.0, 7.0]

@@ -126,17 +126,21 @@ def _sorted_sequence(n_univ, seed):
     return reqs
 
 
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64, psg.F16, psg.BF16])
 @pytest.mark.parametrize("n_univ,seed", [(50, 1), (5000, 2), (300000, 3)])
-def test_sorted_store_vs_oracle(n_univ, seed):
-    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
-    orc = oracle.Store()
-    for flags, k, v in _sorted_sequence(n_univ, seed):
+def test_sorted_store_vs_oracle(n_univ, seed, dtype):
+    """Every dtype through the fused resolve + apply: f32 takes the 16-B vector
+    paths, f64 / f16 / bf16 the scalar ones."""
+    st = psg.Store(psg.SORTED, dtype, 0, KMAX, 0)
+    orc = oracle.Store(dtype)
+    for j, (flags, k, _) in enumerate(_sorted_sequence(n_univ, seed)):
         n = len(k)
-        out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+        v = synth(n, dtype, 1000 * seed + j, 1, -1.0, 1.0)
+        out = psg.DeviceBuffer(n * ES[dtype]) if flags & psg.PULL else None
         st.handle(flags, dev(k), dev(v) if flags & psg.PUSH else None, out, n)
         exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
         if out is not None:
-            np.testing.assert_array_equal(out.download(np.float32, n), exp)
+            np.testing.assert_array_equal(out.download(NPT[dtype], n), exp)
     gk, gv = st.dump()
     ok, ov = orc.dump()
     np.testing.assert_array_equal(gk, ok)  # pulls of absent keys inserted them too
@@ -184,7 +188,9 @@ def test_sorted_resolve_and_slot_requests():
 
 def test_sorted_sparse_requests_use_global_search():
     """A request far sparser than the store leaves windows wider than the LDS
-    window (4096 keys): the resolve falls back to global searches."""
+    window (2 * block * 4 keys: 8192 at the default 1024-thread block): the
+    resolve falls back to global searches.  Stride 10007 over 2 M keys spans
+    ~40 M key positions per 4096-key tile, past the window at any block size."""
     rng = np.random.default_rng(31)
     univ = np.unique(rng.integers(0, 1 << 63, 2_000_000, dtype=np.uint64))
     st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)

@@ -50,7 +50,9 @@ def _xgmi_rank(rank, world, n, steps, name, q_in, q_out):
     _paths()
     import oracle
     import psg
-    psg.set_device(0)
+    # one GPU per rank where the box has them (the reads then cross xGMI); on a
+    # 1-GPU box the ranks share it and the peer reads stay on the card
+    psg.set_device(rank % psg.device_count())
     blk = n // world
     vals = psg.DeviceBuffer(n * 4)
     vals.fill_synth(n, psg.F32, 7 + rank, 0, 0.0, 1000.0)
@@ -141,3 +143,27 @@ def test_bench_n2_shared_gpu_xgmi_verified():
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["parity_check"] is True, res
     assert res["config"].get("xgmi_checksum_verified") is True, res
+
+
+def test_node_barrier_timeout_poisons_and_names_are_exclusive():
+    """A wait that times out breaks the barrier for every rank (its arrival was
+    already counted, so a later wait must not release a phase early), and
+    rank 0 refuses a name whose segment already exists (a crashed job's)."""
+    _paths()
+    import psg
+    name = "psg_test_" + uuid.uuid4().hex[:12]
+    b0 = psg.NodeBarrier(name, 2, 0)
+    b1 = psg.NodeBarrier(name, 2, 1)
+    with pytest.raises(psg.PsgError, match="timed out"):
+        b0.wait(0.05)  # rank 1 never arrives
+    with pytest.raises(psg.PsgError, match="broken"):
+        b1.wait(1.0)
+    with pytest.raises(psg.PsgError, match="broken"):
+        b0.wait(1.0)
+    with pytest.raises(psg.PsgError, match="O_EXCL"):
+        psg.NodeBarrier(name, 2, 0)  # the segment still exists
+    b1.close()
+    b0.close()
+    b2 = psg.NodeBarrier(name, 1, 0)  # unlinked by rank 0's close: the name is free again
+    b2.wait(1.0)
+    b2.close()
