@@ -1,0 +1,36 @@
+#!/bin/bash
+# The one GPU runner: tools/gpu_run.sh STAGE [STAGE ...], run on the box by
+#   gpurun --timeout T -- 'bash tools/gpu_run.sh tests bench prof'
+# Every step has its own time limit; a crash, abort or time-out ends the call
+# (no later GPU step runs).  Outputs land in gpurun_out/.
+#   tests    the whole -m gpu suite            smoke  __graft_entry__.smoke()
+#   bench    default bench line (configs[1])   prof   rocprof kernel stats of it
+#   keyed    keyed bench line (configs[3])     proffk rocprof kernel stats of keyed
+#   f16      1 G f16 bench line (configs[4])   e2e    C++ API end to end, 10 M keys
+#   t:EXPR   pytest -m gpu -k EXPR             pmc:KERNEL:ARGS  PMC traffic passes
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+stop_on_crash() { case "$1" in 124|134|137|139) echo "GPU step crashed/timed out ($1); stopping"; exit "$1";; esac; }
+step() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; stop_on_crash $rc; return $rc; }
+PYT="python3 -u -m pytest -v --timeout 600 --timeout-method thread"
+for st in "$@"; do
+  case "$st" in
+    tests) step 1100 $PYT tests -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "tests rc=$?"; tail -3 gpurun_out/pytest_gpu.log ;;
+    t:*) step 900 $PYT tests -m gpu -k "${st#t:}" > gpurun_out/pytest_k.log 2>&1; echo "tests[${st#t:}] rc=$?"; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_k.log | tail -30 ;;
+    smoke) step 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 gpurun_out/smoke.log ;;
+    bench) step 300 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; echo "bench rc=$?"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err ;;
+    prof) rm -rf gpurun_out/prof64
+          step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof64 -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/prof64.json 2>&1; echo "prof rc=$?"
+          f=$(find gpurun_out/prof64 -name "*kernel_stats.csv" | head -1); cut -c1-200 "$f" | head -12 ;;
+    keyed) step 300 python3 bench.py --workload keyed --no-cpu-baseline > gpurun_out/bench_keyed.json 2> gpurun_out/bench_keyed.err; echo "keyed rc=$?"; cat gpurun_out/bench_keyed.json; tail -3 gpurun_out/bench_keyed.err ;;
+    proffk) rm -rf gpurun_out/prof_keyed
+          step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_keyed -o run --output-format csv -- python3 bench.py --workload keyed --no-cpu-baseline --steps 20 > gpurun_out/prof_keyed.json 2>&1; echo "proffk rc=$?"
+          f=$(find gpurun_out/prof_keyed -name "*kernel_stats.csv" | head -1); cut -c1-200 "$f" | head -12 ;;
+    f16) step 300 python3 bench.py --workload dense-f16 --no-cpu-baseline > gpurun_out/bench_f16.json 2> gpurun_out/bench_f16.err; echo "f16 rc=$?"; cat gpurun_out/bench_f16.json ;;
+    e2e) step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 10000000 20 > gpurun_out/e2e_threads_10M.log 2>&1; echo "e2e threads rc=$?"; head -3 gpurun_out/e2e_threads_10M.log
+         step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 -procs 10000000 20 > gpurun_out/e2e_procs_10M.log 2>&1; echo "e2e procs rc=$?"; head -3 gpurun_out/e2e_procs_10M.log ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done
