@@ -625,12 +625,12 @@ def cpu_baseline(args) -> dict:
     if args.cpu_configs0_keys:
         n0 = args.cpu_configs0_keys
         t0 = time.perf_counter()
-        f0, p0, l0 = oracle.bench(n0, 2)
+        f0, p0, l0 = oracle.bench(n0, 6)
         out["configs0_sample"] = {
             "value": round(2 * 4 * n0 / (p0 + l0) / 1e9, 4), "unit": "GB/s",
             "sample": (f"configs[0] layout: {n0} keys at kMaxKey/num*i "
                        f"(test_kv_app_benchmark.cpp:47-52), 1 inserting Push ({f0:.2f} s) "
-                       f"then 2 steady Push+Pull, {time.perf_counter() - t0:.1f} s"),
+                       f"then 6 steady Push+Pull, {time.perf_counter() - t0:.1f} s"),
         }
     return out
 
@@ -669,7 +669,7 @@ def main(argv=None) -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe256", action="store_true")
     ap.add_argument("--cpu-keys", type=int, default=64 << 20)
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-reps", type=int, default=12)
     ap.add_argument("--cpu-configs0-keys", type=int, default=10_000_000,
                     help="also time configs[0]'s layout at this many keys (0: skip)")
     args = ap.parse_args(argv)
