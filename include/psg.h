@@ -320,6 +320,30 @@ int psg_adam_destroy(psg_adam* a);
  * [0, n).  Bit-identical to the reference's operation order. */
 int psg_lr_apply(psg_store* weights, const float* merged, uint64_t n, float lr,
                  psg_adam* adam, int iteration, psg_stream stream);
+/* The BSP round of LRServer::RequestHandle fused into ONE pass:
+ *   s_i = from_zero ? ((0 + g_0[i]) + g_1[i]) + ... : (g_0[i] + g_1[i]) + ...
+ * (f32 adds in the order given — the arrival order of `merge_buf_.vals[i] +=
+ * req_data.vals[i]`, LRServer.h:158-160; from_zero = 1 for sync mode's merge
+ * buffer, 0 for async mode's single push, LRServer.h:179-189), then the
+ * update of psg_lr_apply on s_i.  No merge buffer is written or cleared.
+ * grads_host: 1..16 device pointers to n floats each. */
+int psg_lr_apply_sum(psg_store* weights, const float* const* grads_host, int ngrads,
+                     int from_zero, uint64_t n, float lr, psg_adam* adam, int iteration,
+                     psg_stream stream);
+/* Multi-GPU LR BSP Push (nw = ns = nranks, weights = rank r's f32 DENSE shard
+ * of n_total / nranks features, adam = that shard's state):
+ *   psg_comm_lr_push  reduce-scatter of every rank's grads[n_total] (RCCL; its
+ *                     summation order, so 1e-6 relative against the reference)
+ *                     into scratch (NULL: the comm's), then the fused apply;
+ *   psg_xgmi_lr_push  ONE kernel reading block r of every rank's registered
+ *                     request vector (the gradients) over xGMI, merged from 0 in
+ *                     rank order and applied (bit-exact against the reference
+ *                     replaying the pushes in rank order).
+ * Pull of the model is psg_comm_pull / psg_xgmi_pull. */
+int psg_comm_lr_push(psg_comm* c, psg_store* weights, const float* grads, uint64_t n_total,
+                     float lr, psg_adam* adam, int iteration, void* scratch, psg_stream stream);
+int psg_xgmi_lr_push(psg_xgmi* x, psg_store* weights, uint64_t n_total, float lr,
+                     psg_adam* adam, int iteration, psg_stream stream);
 
 #ifdef __cplusplus
 }

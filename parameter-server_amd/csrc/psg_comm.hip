@@ -165,6 +165,32 @@ int psg_comm_push(psg_comm* c, psg_store* shard, const void* vals, uint64_t n_to
   return dense_request(shard->dtype, PSG_PUSH, shard->vals, scratch, nullptr, blk, st);
 }
 
+// LR BSP Push over RCCL: the reduce-scatter of every rank's gradient vector,
+// then the fused apply on this rank's weight shard (the merge buffer of
+// LRServer.h:158-160 is the reduce-scatter output; no merge store, no clear).
+int psg_comm_lr_push(psg_comm* c, psg_store* weights, const float* grads, uint64_t n_total, float lr,
+                     psg_adam* adam, int iteration, void* scratch, psg_stream stream) {
+  uint64_t blk = 0;
+  PSG_TRY(check_shard(c, weights, n_total, &blk));
+  if (blk == 0) return PSG_OK;
+  PSG_REQUIRE(grads, PSG_ERR_INVALID, "psg_comm_lr_push: null grads");
+  PSG_REQUIRE(weights->dtype == PSG_F32, PSG_ERR_UNSUPPORTED, "psg_comm_lr_push: f32 weights only");
+  hipStream_t st = (hipStream_t)stream;
+  const float* merged = grads;  // one rank: its own gradient block is the merge
+  if (c->nranks > 1 || c->force) {
+    if (!scratch) {
+      PSG_TRY(ensure_scratch(c, blk * sizeof(float)));
+      scratch = c->scratch;
+    }
+    PSG_NCCL(ncclReduceScatter(grads, scratch, blk, ncclFloat32, ncclSum, c->comm[0], st));
+    merged = (const float*)scratch;
+  } else {
+    merged = grads + (uint64_t)c->rank * blk;
+  }
+  const float* g[1] = {merged};
+  return lr_apply_sum(weights, 0, g, 1, 1, blk, lr, adam, 0, iteration, st);
+}
+
 int psg_comm_pull(psg_comm* c, psg_store* shard, void* out, uint64_t n_total, psg_stream stream) {
   uint64_t blk = 0;
   PSG_TRY(check_shard(c, shard, n_total, &blk));

@@ -144,7 +144,25 @@ struct psg_store {
   int* flags_host;   // pinned host int[4]: any key absent / non-contiguous / out of range / unsorted
 };
 
+struct psg_adam {
+  uint64_t n;
+  double lr, beta1, beta2, eps;
+  double* m;  // n doubles each (Adam.h:40-41), 16-B aligned (hipMalloc)
+  double* v;
+};
+
 namespace psg {
+// Gradient arrays one LR apply pass merges (LRServer's BSP round: one per worker).
+constexpr int kMaxGrads = 16;
+struct Grads {
+  const float* p[kMaxGrads];
+};
+// weights[w_off + i] -= update(sum_k grads[k][i]) for i < n, Adam state at
+// adam_off; the merge and the apply of LRServer.h:158-177 in one pass.
+// psg_lr.hip.
+int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, int ngrads,
+                 int from_zero, uint64_t n, float lr, psg_adam* adam, uint64_t adam_off,
+                 int iteration, hipStream_t st);
 // Dense element-wise request on slot range [off, off + n) of a store value
 // array.  op = PSG_PUSH | PSG_PULL bits.  Implemented in psg_dense.hip.
 int dense_request(int dtype, int op, void* store_vals, const void* vals, void* out,

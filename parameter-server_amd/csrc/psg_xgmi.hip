@@ -181,6 +181,24 @@ int psg_xgmi_push(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream st
   return PSG_OK;
 }
 
+// LR BSP Push over xGMI: rank r reads block r of every rank's gradient vector
+// (N-1 of them over the links) and applies the merged gradient to its weight
+// shard in ONE kernel — merge from 0 in rank order (one arrival order of
+// LRServer.h:158-160), then SGD / Adam (LRServer.h:171-177).
+int psg_xgmi_lr_push(psg_xgmi* x, psg_store* weights, uint64_t n_total, float lr, psg_adam* adam,
+                     int iteration, psg_stream stream) {
+  PSG_REQUIRE(x && weights && weights->kind == PSG_STORE_DENSE && weights->dtype == PSG_F32,
+              PSG_ERR_INVALID, "psg_xgmi_lr_push: need an f32 DENSE weight shard");
+  PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_lr_push: n_total %% nranks");
+  PSG_REQUIRE(weights->vals == x->stores[x->rank], PSG_ERR_INVALID,
+              "psg_xgmi_lr_push: weights are not this rank's registered shard");
+  PSG_REQUIRE(x->nranks <= kMaxGrads, PSG_ERR_INVALID, "psg_xgmi_lr_push: at most %d ranks", kMaxGrads);
+  const uint64_t blk = n_total / (uint64_t)x->nranks;
+  const float* g[kMaxPeers];
+  for (int w = 0; w < x->nranks; ++w) g[w] = (const float*)x->vals[w] + (uint64_t)x->rank * blk;
+  return lr_apply_sum(weights, 0, g, x->nranks, 1, blk, lr, adam, 0, iteration, (hipStream_t)stream);
+}
+
 int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream) {
   PSG_REQUIRE(x && shard && out, PSG_ERR_INVALID, "psg_xgmi_pull: null argument");
   PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_pull: n_total %% nranks");

@@ -45,7 +45,8 @@ EXPORTS = [
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
-    "psg_adam_create", "psg_adam_destroy", "psg_lr_apply",
+    "psg_adam_create", "psg_adam_destroy", "psg_lr_apply", "psg_lr_apply_sum",
+    "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
     "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_node_barrier_create",
     "psg_node_barrier_wait", "psg_node_barrier_destroy",
@@ -122,6 +123,9 @@ def lib() -> C.CDLL:
             "psg_adam_create": ([u64, f64, f64, f64, f64, C.POINTER(vp)], i32),
             "psg_adam_destroy": ([vp], i32),
             "psg_lr_apply": ([vp, vp, u64, f32, vp, i32, vp], i32),
+            "psg_lr_apply_sum": ([vp, C.POINTER(vp), i32, i32, u64, f32, vp, i32, vp], i32),
+            "psg_comm_lr_push": ([vp, vp, vp, u64, f32, vp, i32, vp, vp], i32),
+            "psg_xgmi_lr_push": ([vp, vp, u64, f32, vp, i32, vp], i32),
             "psg_ipc_handle_bytes": ([], i32), "psg_ipc_export": ([vp, vp], i32),
             "psg_ipc_export_range": ([vp, vp, C.POINTER(u64)], i32),
             "psg_ipc_open": ([vp, C.POINTER(vp)], i32), "psg_ipc_close": ([vp], i32),
@@ -404,6 +408,11 @@ class Comm:
         _call("psg_comm_push_keyed", self.h, shard.h, _ptr(keys), _ptr(vals), n,
               kp.ctypes.data_as(C.c_void_p), _s(stream))
 
+    def lr_push(self, weights: Store, grads, n_total: int, lr: float, adam=None, iteration=0,
+                scratch=None, stream=None) -> None:
+        _call("psg_comm_lr_push", self.h, weights.h, _ptr(grads), n_total, lr,
+              adam.h if adam else None, iteration, _ptr(scratch), _s(stream))
+
     def pull_keyed(self, shard: Store, keys, out, n: int, key_pos, stream=None) -> None:
         kp = np.ascontiguousarray(key_pos, dtype=np.uint64)
         _call("psg_comm_pull_keyed", self.h, shard.h, _ptr(keys), _ptr(out), n,
@@ -431,6 +440,14 @@ def lr_apply(weights: Store, merged, n: int, lr: float, adam: Adam | None, itera
              stream=None) -> None:
     _call("psg_lr_apply", weights.h, _ptr(merged), n, lr, adam.h if adam else None, iteration,
           _s(stream))
+
+
+def lr_apply_sum(weights: Store, grads, n: int, lr: float, adam: Adam | None, iteration: int,
+                 from_zero: bool = True, stream=None) -> None:
+    """psg_lr_apply_sum: merge `grads` (device buffers / pointers, in order) and apply."""
+    arr = (C.c_void_p * max(len(grads), 1))(*[_ptr(g) for g in grads])
+    _call("psg_lr_apply_sum", weights.h, arr, len(grads), int(from_zero), n, lr,
+          adam.h if adam else None, iteration, _s(stream))
 
 
 # ---- one-shot xGMI exchange ----------------------------------------------------------
@@ -465,6 +482,11 @@ class Xgmi:
 
     def pull(self, shard: Store, out, n_total: int, stream=None) -> None:
         _call("psg_xgmi_pull", self.h, shard.h, _ptr(out), n_total, _s(stream))
+
+    def lr_push(self, weights: Store, n_total: int, lr: float, adam=None, iteration=0,
+                stream=None) -> None:
+        _call("psg_xgmi_lr_push", self.h, weights.h, n_total, lr, adam.h if adam else None,
+              iteration, _s(stream))
 
     def close(self) -> None:
         if self.h.value:

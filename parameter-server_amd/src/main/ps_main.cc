@@ -1,5 +1,6 @@
-// ps_main.cc — the launcher: links under a PS program whose main() was
-// compiled as ps_user_main (-Dmain=ps_user_main).  Three ways to run:
+// ps_main.cc — the launcher: links under a PS program whose main() symbol
+// was renamed ps_user_main in its object file (objcopy --redefine-sym
+// main=ps_user_main; see PS_BUILD in the Makefile).  Three ways to run:
 //
 //   ./prog config.json log.txt <role> [args]   one node of a multi-process job,
 //        exactly the command line tests/local.py gives a node (local.py:87-114);
@@ -16,7 +17,8 @@
 
 #include "internal/PostOffice.h"
 
-int ps_user_main(int argc, char** argv);
+// the program's own main(), renamed: an unmangled symbol, so C linkage here
+extern "C" int ps_user_main(int argc, char** argv);
 
 int main(int argc, char** argv) {
   if (ps::proc::RoleOf(argc, argv)) return ps::proc::RunNode(ps_user_main, argc, argv);

@@ -6,7 +6,10 @@
 // are dyadic (multiples of 1/64), so their sum is exact in any arrival order
 // and the final model can be compared bit for bit with a replay of the
 // reference's update (LRServer.h:171-177, Adam.h:28-34) done here on the CPU.
-// usage: lr_sync_gpu [-ns 1] [-nw W] sync(0|1) adam(0|1) epochs batches features
+// With key_cache = 1 the server caches key lists and the workers send the
+// list's hash after their first request (USE_KEY_CACHING: LRServer.h:127-142,
+// LRWorker.h:214-219).
+// usage: lr_sync_gpu [-ns 1] [-nw W] sync(0|1) adam(0|1) epochs batches features [key_cache]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -28,13 +31,14 @@ int main(int argc, char* argv[]) {
   const int epochs = argc > 6 ? std::atoi(argv[6]) : 3;
   const int batches = argc > 7 ? std::atoi(argv[7]) : 4;
   const int n = argc > 8 ? std::atoi(argv[8]) : 123;
+  const bool key_cache = argc > 9 ? std::atoi(argv[9]) != 0 : false;
   const float lr = 0.01f;
   std::vector<float> w0(n);
   for (int i = 0; i < n; ++i) w0[i] = (float)((i % 13) - 6) / 16.0f;
 
   if (IsServer()) {
     auto server = new KVServer<float>(0);
-    server->SetDeviceRequestHandle(KVServerLRHandle(w0, lr, sync_mode == 0, use_adam));
+    server->SetDeviceRequestHandle(KVServerLRHandle(w0, lr, sync_mode == 0, use_adam, 0, key_cache));
     RegisterExitCallback([server]() { delete server; });
   }
   if (IsWorker()) {
@@ -46,6 +50,11 @@ int main(int argc, char* argv[]) {
     for (int e = 0; e < epochs; ++e) {
       for (int b = 0; b < batches; ++b) {
         kv.Wait(kv.Pull(keys, &w));
+        if (key_cache && keys.size() > 1) {  // LRWorker::CacheKey (LRWorker.h:214-219)
+          const Key h = detail::KeyListHash(keys.data(), keys.size());
+          keys = std::vector<Key>{h};
+        }
+        CHECK_EQ(w.size(), (size_t)n);
         for (int i = 0; i < n; ++i) g[i] = grad_of(rank, e, b, i);
         kv.Wait(kv.Push(keys, g, {}, b == batches - 1 ? 1 : 0));
       }

@@ -166,3 +166,63 @@ def test_socket_group_collectives(world):
         assert ag == [(r, b"h" * r) for r in range(world)]
         assert bc == {"uid": b"\x01\x02"}
         assert mx == [float(world - 1), 0.0, 7.0]
+
+
+def _lr_rank(rank, world, port, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch
+    import torch.distributed as dist
+    import oracle
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    n, rounds = 6000, 4
+    blk = n // world
+    w = oracle.synth(blk, oracle.F32, 900 + rank, 1, -0.5, 0.5)
+    m, v = np.zeros(blk), np.zeros(blk)
+    out = torch.zeros(n)
+    for it in range(rounds):
+        g = torch.from_numpy(oracle.synth(n, oracle.F32, 1000 * it + rank, 1, -1.0, 1.0))
+        merged = torch.zeros(blk)
+        dist.reduce_scatter_tensor(merged, g)  # psg_comm_lr_push's collective
+        oracle.lr_apply(w, merged.numpy().astype(np.float32), 0.01, m, v, float(np.float32(0.01)),
+                        0.9, 0.999, 1e-8, it)
+        dist.all_gather_into_tensor(out, torch.from_numpy(w))
+    np.save(os.path.join(outdir, f"lr{rank}.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_lr_bsp_reduce_scatter_within_tolerance(world):
+    """The LR BSP round as the multi-GPU path runs it (reduce-scatter of the
+    workers' gradients, the SGD/Adam update on each shard, all-gather of the
+    model), rehearsed on gloo, against the reference replayed with every
+    worker's push merged in arrival order: the collective sums in its own
+    order, so the bar is the north star's 1e-6 relative."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as d:
+        port = _free_port()
+        procs = [ctx.Process(target=_lr_rank, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+        assert all(p.exitcode == 0 for p in procs)
+        got = [np.load(os.path.join(d, f"lr{r}.npy")) for r in range(world)]
+    n, rounds = 6000, 4
+    blk = n // world
+    exp = np.empty(n, np.float32)
+    for s in range(world):
+        w = oracle.synth(blk, oracle.F32, 900 + s, 1, -0.5, 0.5)
+        m, v = np.zeros(blk), np.zeros(blk)
+        for it in range(rounds):
+            merged = np.zeros(blk, np.float32)
+            for r in range(world):
+                merged = (merged + oracle.synth(n, oracle.F32, 1000 * it + r, 1, -1.0, 1.0)[s * blk:(s + 1) * blk]
+                          ).astype(np.float32)
+            oracle.lr_apply(w, merged, 0.01, m, v, float(np.float32(0.01)), 0.9, 0.999, 1e-8, it)
+        exp[s * blk:(s + 1) * blk] = w
+    for r in range(world):
+        assert np.all(np.abs(got[r] - exp) <= REL_TOL * np.abs(exp) + 1e-7), r
