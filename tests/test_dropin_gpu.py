@@ -69,12 +69,15 @@ def test_reference_benchmark_runs():
 
 
 @pytest.mark.parametrize("nw,sync,adam,cache", [(1, 0, 0, 0), (1, 0, 1, 0), (3, 0, 0, 0), (1, 1, 1, 0),
-                                                (3, 0, 1, 1), (2, 1, 0, 1), (18, 0, 1, 0)])
+                                                (3, 0, 1, 1), (1, 1, 0, 1), (18, 0, 1, 0),
+                                                (18, 0, 0, 1)])
 def test_lr_server_in_hbm_matches_reference_update(nw, sync, adam, cache):
     """KVServerLRHandle (BSP merge + SGD/Adam fused into one kernel per round on
     the GPU) vs a replay of LRServer.h:151-189 / Adam.h:28-34, bit for bit
     (tests/harness/lr_sync_gpu.cpp); `cache` runs the key-cache protocol
-    (LRServer.h:127-142); 18 workers exceed one pass's 16 gradient frames."""
+    (LRServer.h:127-142); 18 workers exceed one pass's 16 gradient frames.
+    Async mode runs one worker: with several, their updates interleave in
+    arrival order and round differently (as in the reference)."""
     exe = os.path.join(BIN, "lr_sync_gpu")
     _need(exe)
     r = run(exe, "-ns", 1, "-nw", nw, sync, adam, 3, 4, 123, cache)

@@ -115,6 +115,15 @@ def test_comm_lr_push_single_rank(force, adam, monkeypatch):
 
 
 def _xgmi_lr_rank(rank, world, n, rounds, adam, name, q_in, q_out):
+    try:
+        _xgmi_lr_rank_body(rank, world, n, rounds, adam, name, q_in, q_out)
+    except BaseException:  # report instead of leaving the peers and the parent waiting
+        import traceback
+        q_out.put(("err", rank, traceback.format_exc()))
+        raise
+
+
+def _xgmi_lr_rank_body(rank, world, n, rounds, adam, name, q_in, q_out):
     for p in (os.path.join(ROOT, "parameter-server_amd", "python"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     import psg
@@ -129,7 +138,7 @@ def _xgmi_lr_rank(rank, world, n, rounds, adam, name, q_in, q_out):
     sptr = w.info().vals
     psg.device_sync()
     q_out.put(("h", rank, psg.ipc_export(grads.ptr), psg.ipc_export(sptr)))
-    handles = q_in.get(timeout=120)
+    handles = q_in.get(timeout=60)
     gptrs = [grads.ptr if r == rank else psg.ipc_open(handles[r][0]) for r in range(world)]
     sptrs = [sptr if r == rank else psg.ipc_open(handles[r][1]) for r in range(world)]
     x = psg.Xgmi(world, rank, gptrs, sptrs)
@@ -138,15 +147,15 @@ def _xgmi_lr_rank(rank, world, n, rounds, adam, name, q_in, q_out):
     for it in range(rounds):
         grads.fill_synth(n, psg.F32, 1000 * it + rank, 1, -1.0, 1.0)
         psg.device_sync()
-        bar.wait()  # every rank's gradient is written
+        bar.wait(30.0)  # every rank's gradient is written
         x.lr_push(w, n, 0.01, a, it)
         psg.device_sync()
-        bar.wait()  # every shard is updated
+        bar.wait(30.0)  # every shard is updated
         x.pull(w, out, n)
         psg.device_sync()
-        bar.wait()  # nobody overwrites a gradient a peer still reads
+        bar.wait(30.0)  # nobody overwrites a gradient a peer still reads
     got = out.download(np.float32, n)
-    bar.wait()
+    bar.wait(30.0)
     x.close()
     for r in range(world):
         if r != rank:
@@ -168,18 +177,27 @@ def test_xgmi_lr_push_multiprocess(world, adam):
              for r in range(world)]
     for p in procs:
         p.start()
-    handles = {}
-    for _ in range(world):
-        _, r, hg, hs = q_out.get(timeout=240)
-        handles[r] = (hg, hs)
-    for r in range(world):
-        q_in[r].put(handles)
-    results = {}
-    for _ in range(world):
-        _, r, got = q_out.get(timeout=240)
-        results[r] = got
-    for p in procs:
-        p.join(60)
+    def get():
+        msg = q_out.get(timeout=100)
+        assert msg[0] != "err", f"rank {msg[1]} failed:\n{msg[2]}"
+        return msg
+
+    try:
+        handles = {}
+        for _ in range(world):
+            _, r, hg, hs = get()
+            handles[r] = (hg, hs)
+        for r in range(world):
+            q_in[r].put(handles)
+        results = {}
+        for _ in range(world):
+            _, r, got = get()
+            results[r] = got
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     blk = n // world
     w0 = np.concatenate([oracle.synth(blk, oracle.F32, 900 + r, 1, -0.5, 0.5) for r in range(world)])

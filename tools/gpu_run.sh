@@ -14,7 +14,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop_on_crash() { case "$1" in 124|134|137|139) echo "GPU step crashed/timed out ($1); stopping"; exit "$1";; esac; }
 step() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; stop_on_crash $rc; return $rc; }
-PYT="python3 -u -m pytest -v --timeout 600 --timeout-method thread"
+PYT="python3 -u -m pytest -v --timeout 150 --timeout-method thread"
 for st in "$@"; do
   case "$st" in
     tests) step 1100 $PYT tests -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "tests rc=$?"; tail -3 gpurun_out/pytest_gpu.log ;;
