@@ -141,7 +141,12 @@ struct psg_store {
   uint64_t* wlo;     // per-tile store-key windows of the resolve
   uint64_t slots_cap;
   int* flags;        // device view of flags_host: the kernels raise flags there
-  int* flags_host;   // pinned host int[4]: any key absent / non-contiguous / out of range / unsorted
+  int* flags_host;   // pinned host int[4]: any key absent / out of range / unsorted
+  // Device word the validation pass sets to the request's sequence number when
+  // the request is invalid (unsorted, duplicate or out-of-range keys); every
+  // store-writing kernel of that request reads it first and writes nothing.
+  int* reject_dev;
+  int seq;           // request sequence number (never 0 after the first request)
 };
 
 struct psg_adam {

@@ -8,16 +8,22 @@
 //           (psg_dense.hip).
 //   SORTED  a sorted uint64 key array K[0..size) and a value array V in the
 //           same order.  A request (sorted, unique keys — the KVPairs contract,
-//           KVApp.h:23) is resolved to slots by a block-narrowed lower_bound:
-//           each block takes a 1024-key tile, finds the window of K its first
-//           and last key bracket, and every lane binary-searches inside that
-//           window (L2-resident when the request is dense in K).  When the
-//           resolved slots are one contiguous run (the steady state of a worker
-//           that pushes the same key set, test_kv_app*.cpp, LR_ps) the request
-//           runs as the dense streaming kernel on V + slot0.  Keys that are
-//           absent are inserted with value 0 before the request is applied —
-//           the `operator[]` insert of KVApp.h:449/452 — by a parallel merge of
-//           the (compacted, sorted) new keys into K and V.
+//           KVApp.h:23) runs as two kernels:
+//             k_validate_windows  reads every request key once (coalesced):
+//               strictly ascending and inside the shard's range, or the whole
+//               request is rejected before anything is written; and, per
+//               request tile, the window of K its first and last key bracket
+//               (one 64-ary search per tile end);
+//             k_resolve_apply     stages each tile's window of K into LDS,
+//               places every key by an LDS search / merge walk and applies the
+//               request to the found slots (store[slot] += val, out = store).
+//           Keys that are absent are inserted with value 0 afterwards — the
+//           `operator[]` insert of KVApp.h:449/452 — by a parallel merge of the
+//           (compacted, sorted) new keys into K and V, and the request is
+//           applied to exactly those keys.
+//   Rejected requests (unsorted, duplicate, out-of-range keys) leave the store
+//   unchanged: the validation pass raises a device word that every
+//   store-writing kernel of the request checks first.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -33,7 +39,7 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // (one plain store of 1 per wave that saw the condition — idempotent, no
 // atomics), so a request needs no flag reset launch and no flag copy: the
 // host zeroes them before the launch and reads them after the stream sync.
-enum { F_MISSING = 0, F_NONCONTIG = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
+enum { F_MISSING = 0, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
 
 __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
   if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
@@ -111,9 +117,9 @@ __device__ __forceinline__ uint32_t lower_bound_lds(const uint64_t* a, uint32_t 
 // it is almost always at the previous position or the one after, two LDS
 // reads — with a binary search of the rest of the window as the fallback.  A
 // global search is used only when a sparse request leaves a window wider than
-// kWin.  slots[i] = index of q[i] in K, or kNoSlot.  flags: [F_MISSING] +=
-// absent keys, [F_NONCONTIG] |= slots not equal to base + i, [F_RANGE] |= key
-// outside [kb, ke), [F_UNSORTED] |= q not strictly ascending.  A slot is only
+// kWin.  slots[i] = index of q[i] in K, or kNoSlot.  flags: [F_MISSING] |=
+// absent keys, [F_RANGE] |= key outside [kb, ke), [F_UNSORTED] |= q not
+// strictly ascending.  A slot is only
 // written when K[slot] == key, so unsorted input never produces a wrong slot
 // (it is flagged and the request rejected).
 constexpr int kPerLane = kTile / kBlock;  // 4 consecutive keys per lane
@@ -124,9 +130,8 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
                                                  uint64_t ke, uint32_t* __restrict__ slots,
                                                  int* __restrict__ flags) {
   __shared__ uint64_t sK[kWin];
-  int missing = 0, noncontig = 0, range = 0, unsorted = 0;
+  int missing = 0, range = 0, unsorted = 0;
   const uint64_t ntiles = (n + kTile - 1) / kTile;
-  const uint64_t base = wlo[0];
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * kTile;
     const uint64_t t1 = (t0 + kTile < n) ? t0 + kTile : n;
@@ -170,7 +175,6 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
       }
       out[k] = found ? (uint32_t)p : kNoSlot;
       if (!found) missing++;
-      if (!found || p != base + i) noncontig = 1;
     }
     if (i0 + kPerLane <= t1 && ((i0 & 3) == 0)) {
       // 16-B store of the lane's 4 slots (slots is our own 256-B aligned buffer)
@@ -182,7 +186,85 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
     __syncthreads();
   }
   raise_flag(flags, F_MISSING, missing != 0);
-  raise_flag(flags, F_NONCONTIG, noncontig != 0);
+  raise_flag(flags, F_RANGE, range != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
+}
+
+// Pass 1 of a SORTED request: validate the whole request and find each
+// tile's window of K.  One block per request tile of NT * 4 keys (the tile of
+// k_resolve_apply): every lane loads its 4 keys (16-B loads) and the key
+// before them, and checks strict ascent and the shard's range [kb, ke); wave 0
+// finds wlo[tile] = lower_bound(K, q[t0]) and, in the last tile, wave 1 finds
+// wlo[ntiles] = lower_bound(K, q[n - 1]) + 1.  An invalid request sets
+// *reject = seq, which k_resolve_apply checks before it writes anything, and
+// raises F_UNSORTED / F_RANGE for the host.  Bytes: the request keys once
+// (8 B / key; k_resolve_apply's re-read of them right after is served mostly
+// by the Infinity Cache) plus ~4 scattered 512-B probes per tile end.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_validate_windows(const uint64_t* __restrict__ q, uint64_t n,
+                                                         const uint64_t* __restrict__ K, uint64_t S,
+                                                         uint64_t* __restrict__ wlo, uint64_t kb,
+                                                         uint64_t ke, int* __restrict__ reject, int seq,
+                                                         int* __restrict__ flags, int vec) {
+  constexpr uint64_t tileN = (uint64_t)NT * kPerLane;
+  int range = 0, unsorted = 0;
+  const uint64_t ntiles = (n + tileN - 1) / tileN;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * tileN;
+    const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
+    const int wave = threadIdx.x >> 6;
+    if (wave == 0) {
+      const uint64_t r = lower_bound_wave(K, S, q[t0]);
+      if ((threadIdx.x & 63) == 0) wlo[tile] = r;
+    } else if (wave == 1 && tile + 1 == ntiles) {
+      const uint64_t h = lower_bound_wave(K, S, q[n - 1]);
+      if ((threadIdx.x & 63) == 0) wlo[ntiles] = h < S ? h + 1 : S;
+    }
+    const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
+    if (i0 < t1) {
+      uint64_t key[kPerLane];
+      if (i0 + kPerLane <= t1 && vec) {
+        const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0));
+        const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0 + 2));
+        key[0] = a[0];
+        key[1] = a[1];
+        key[2] = b[0];
+        key[3] = b[1];
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : ~0ull;
+      }
+      uint64_t prev = i0 > 0 ? q[i0 - 1] : 0;
+      bool first = i0 == 0;
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        if (i0 + k >= t1) break;
+        if (key[k] < kb || key[k] >= ke) range = 1;
+        if (!first && prev >= key[k]) unsorted = 1;
+        prev = key[k];
+        first = false;
+      }
+    }
+  }
+  const bool bad = range || unsorted;
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) *reject = seq;
+  raise_flag(flags, F_RANGE, range != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
+}
+
+// DENSE store addressed by explicit keys: the same request validation (keys
+// strictly ascending, inside [kb, kb + cap)) before any slot is written.
+__global__ __launch_bounds__(256) void k_validate_keys(const uint64_t* __restrict__ q, uint64_t n,
+                                                       uint64_t kb, uint64_t cap, int* __restrict__ reject,
+                                                       int seq, int* __restrict__ flags) {
+  int range = 0, unsorted = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t key = q[i];
+    if (i > 0 && q[i - 1] >= key) unsorted = 1;
+    if (key < kb || key - kb >= cap) range = 1;
+  }
+  if (__ballot(range || unsorted) && (threadIdx.x & 63) == 0) *reject = seq;
   raise_flag(flags, F_RANGE, range != 0);
   raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
@@ -201,13 +283,17 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
                                                        typename Elem<DT>::T* __restrict__ V,
                                                        const typename Elem<DT>::T* __restrict__ vals,
                                                        typename Elem<DT>::T* __restrict__ outv,
+                                                       const int* __restrict__ reject, int seq,
                                                        int* __restrict__ flags, int vec) {
   using E = Elem<DT>;
   using T = typename E::T;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
   constexpr uint32_t winN = 2 * NT * kPerLane;          // LDS window of store keys
   __shared__ uint64_t sK[winN];
-  int missing = 0, range = 0, unsorted = 0;
+  // k_validate_windows rejected the request: write nothing (a uniform early
+  // exit of every block before any store access)
+  if (*reject == seq) return;
+  int missing = 0;
   const uint64_t ntiles = (n + tileN - 1) / tileN;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * tileN;
@@ -251,7 +337,6 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : 0;
     }
-    uint64_t prev = i0 > 0 && i0 < t1 ? q[i0 - 1] : 0;
     T v[kPerLane];
     if constexpr ((OP & PSG_PUSH) != 0) {
       if constexpr (sizeof(T) == 4) {
@@ -284,9 +369,6 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
       slot[k] = 0;
       if (i >= t1) continue;
       const uint64_t kk = key[k];
-      if (kk < kb || kk >= ke) range = 1;
-      if (i > 0 && prev >= kk) unsorted = 1;
-      prev = kk;
       uint64_t p;
       bool found;
       if (staged) {
@@ -360,8 +442,6 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
     __syncthreads();
   }
   raise_flag(flags, F_MISSING, missing != 0);
-  raise_flag(flags, F_RANGE, range != 0);
-  raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
 
 // Block-wide exclusive scan helper over 256 lanes (wave = 64).
@@ -480,18 +560,13 @@ __global__ __launch_bounds__(256) void k_dense_keyed(typename Elem<DT>::T* __res
                                                      const uint64_t* __restrict__ keys,
                                                      const typename Elem<DT>::T* __restrict__ vals,
                                                      typename Elem<DT>::T* __restrict__ out,
-                                                     uint64_t n, int* __restrict__ flags) {
+                                                     uint64_t n, const int* __restrict__ reject,
+                                                     int seq) {
   using E = Elem<DT>;
-  int bad = 0, unsorted = 0;
+  if (*reject == seq) return;  // k_validate_keys rejected the request
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t key = keys[i];
-    if (i > 0 && keys[i - 1] >= key) unsorted = 1;
-    const uint64_t p = key - kb;  // wraps for key < kb
-    if (key < kb || p >= cap) {
-      bad = 1;
-      continue;
-    }
+    const uint64_t p = keys[i] - kb;
     typename E::T s = store[p];
     if constexpr ((OP & PSG_PUSH) != 0) {
       s = E::add1(s, vals[i]);
@@ -499,8 +574,6 @@ __global__ __launch_bounds__(256) void k_dense_keyed(typename Elem<DT>::T* __res
     }
     if constexpr ((OP & PSG_PULL) != 0) out[i] = s;
   }
-  raise_flag(flags, F_RANGE, bad != 0);
-  raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
 
 // Slots of a DENSE store: key - key_begin (kNoSlot when outside).
@@ -706,24 +779,43 @@ static void launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, co
   if (nt == 1024)
     k_resolve_apply<DT, OP, 1024><<<grid_n(ntiles, 1), 1024, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
                                                                      s->key_end, (T*)s->vals, (const T*)vals,
-                                                                     (T*)out, s->flags, vec);
+                                                                     (T*)out, s->reject_dev, s->seq, s->flags, vec);
   else if (nt == 512)
     k_resolve_apply<DT, OP, 512><<<grid_n(ntiles, 1), 512, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
                                                                    s->key_end, (T*)s->vals, (const T*)vals,
-                                                                   (T*)out, s->flags, vec);
+                                                                   (T*)out, s->reject_dev, s->seq, s->flags, vec);
   else
     k_resolve_apply<DT, OP, 256><<<grid_n(ntiles, 1), 256, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
                                                                    s->key_end, (T*)s->vals, (const T*)vals,
-                                                                   (T*)out, s->flags, vec);
+                                                                   (T*)out, s->reject_dev, s->seq, s->flags, vec);
+}
+
+// A new request: its sequence number tags the reject word (never reset: a
+// stale value names an older request).
+static int next_seq(psg_store* s) {
+  s->seq = s->seq == 0x7fffffff ? 1 : s->seq + 1;
+  return s->seq;
 }
 
 template <int DT>
 static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals,
                          void* out, hipStream_t st) {
-  const uint64_t tile = (uint64_t)ra_block() * kPerLane;
+  const int nt = ra_block();
+  const uint64_t tile = (uint64_t)nt * kPerLane;
   const uint64_t ntiles = (n + tile - 1) / tile;
   reset_flags(s);
-  k_tile_windows<<<grid_n(ntiles + 1, kBlock / 64), kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, tile);
+  const int seq = next_seq(s);
+  const int vk = aligned16(q) ? 1 : 0;
+  const unsigned g = grid_n(ntiles, 1);
+  if (nt == 1024)
+    k_validate_windows<1024><<<g, 1024, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin, s->key_end,
+                                                 s->reject_dev, seq, s->flags, vk);
+  else if (nt == 512)
+    k_validate_windows<512><<<g, 512, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin, s->key_end,
+                                               s->reject_dev, seq, s->flags, vk);
+  else
+    k_validate_windows<256><<<g, 256, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin, s->key_end,
+                                               s->reject_dev, seq, s->flags, vk);
   switch (op) {
     case PSG_PUSH: launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, st); break;
     case PSG_PULL: launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, st); break;
@@ -753,11 +845,15 @@ static int sorted_request(psg_store* s, int op, const uint64_t* q, const void* v
       default: PSG_TRY(resolve_apply<PSG_BF16>(s, op, q, n, vals, out, st)); break;
     }
   } else {
+    // two-pass form (an empty store, or the A/B switch): the flags are read
+    // before the slot pass writes anything
     PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+    PSG_TRY(read_flags(s, st));
+    PSG_TRY(check_request_flags(s));
     PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
   }
   PSG_TRY(read_flags(s, st));
-  PSG_TRY(check_request_flags(s));
+  PSG_TRY(check_request_flags(s));  // rejected by k_validate_windows: nothing was written
   if (s->flags_host[F_MISSING] == 0) return PSG_OK;
   if (sorted_fused() && s->size > 0) {
     // the fused pass kept no slots: resolve again (the keys have not changed)
@@ -796,18 +892,21 @@ static int run_dense_keyed(psg_store* s, int op, const uint64_t* keys, const voi
                            uint64_t n, hipStream_t st) {
   using T = typename Elem<DT>::T;
   unsigned g = grid_n(n, kBlock);
+  const int seq = next_seq(s);
+  // validate the whole request first; the apply writes nothing if it failed
+  k_validate_keys<<<g, kBlock, 0, st>>>(keys, n, s->key_begin, s->capacity, s->reject_dev, seq, s->flags);
   switch (op) {
     case PSG_PUSH:
       k_dense_keyed<DT, PSG_PUSH><<<g, kBlock, 0, st>>>((T*)s->vals, s->key_begin, s->capacity, keys,
-                                                        (const T*)vals, (T*)out, n, s->flags);
+                                                        (const T*)vals, (T*)out, n, s->reject_dev, seq);
       break;
     case PSG_PULL:
       k_dense_keyed<DT, PSG_PULL><<<g, kBlock, 0, st>>>((T*)s->vals, s->key_begin, s->capacity, keys,
-                                                        (const T*)vals, (T*)out, n, s->flags);
+                                                        (const T*)vals, (T*)out, n, s->reject_dev, seq);
       break;
     default:
       k_dense_keyed<DT, PSG_PUSH | PSG_PULL><<<g, kBlock, 0, st>>>(
-          (T*)s->vals, s->key_begin, s->capacity, keys, (const T*)vals, (T*)out, n, s->flags);
+          (T*)s->vals, s->key_begin, s->capacity, keys, (const T*)vals, (T*)out, n, s->reject_dev, seq);
   }
   PSG_HIP(hipGetLastError());
   return PSG_OK;
@@ -851,6 +950,9 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
   if ((e = hipHostGetDevicePointer((void**)&s->flags, s->flags_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(flags)", __FILE__, __LINE__));
   memset(s->flags_host, 0, F_NFLAGS * sizeof(int));
+  if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
+      (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(reject word)", __FILE__, __LINE__));
   if (kind == PSG_STORE_DENSE) {
     s->capacity = capacity;
     s->size = capacity;
@@ -882,6 +984,7 @@ int psg_store_destroy(psg_store* s) {
   if (s->slots2) (void)hipFree(s->slots2);
   if (s->wlo) (void)hipFree(s->wlo);
   if (s->flags_host) (void)hipHostFree(s->flags_host);
+  if (s->reject_dev) (void)hipFree(s->reject_dev);
   delete s;
   return PSG_OK;
 }
@@ -940,7 +1043,8 @@ int psg_store_handle(psg_store* s, int flags, const uint64_t* keys, uint64_t fir
     PSG_REQUIRE(!s->flags_host[F_UNSORTED], PSG_ERR_INVALID,
                 "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
     PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE,
-                "request key outside the DENSE store slots (values of in-range keys applied)");
+                "request key outside the DENSE store slots [%llu, +%llu) (nothing applied)",
+                (unsigned long long)s->key_begin, (unsigned long long)s->capacity);
     return PSG_OK;
   }
   // SORTED

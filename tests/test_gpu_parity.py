@@ -232,6 +232,97 @@ def test_sorted_rejects_duplicate_keys():
     assert ei.value.code == 1 and "ascending" in str(ei.value)
 
 
+@pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL])
+@pytest.mark.parametrize("bad", ["duplicate_last_tile", "unsorted_middle", "out_of_range_last",
+                                 "duplicate_adjacent_lanes"])
+def test_sorted_rejected_request_leaves_a_populated_store_unchanged(bad, flags):
+    """The KVPairs contract (KVApp.h:23): keys strictly ascending.  A request that
+    breaks it — or names a key outside the shard — is rejected as a whole
+    (k_validate_windows runs over every key before k_resolve_apply writes), so
+    the store keeps exactly what it held, even when the bad key sits in the
+    last of many request tiles."""
+    rng = np.random.default_rng(41)
+    kb, ke = 1000, 1 << 62
+    univ = np.unique(rng.integers(kb, ke, 60000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, psg.F32, kb, ke, 0)
+    st.handle(psg.PUSH, dev(univ), dev(rng.uniform(-1, 1, len(univ)).astype(np.float32)), None, len(univ))
+    k0, v0 = st.dump()
+    k = univ.copy()
+    if bad == "duplicate_last_tile":
+        k[-3] = k[-4]
+    elif bad == "unsorted_middle":
+        k[30000], k[30001] = k[30001], k[30000]
+    elif bad == "out_of_range_last":
+        k[-1] = ke + 5
+    else:
+        k[4100] = k[4099]  # the last key of lane 0 and the first of lane 1, second tile
+    n = len(k)
+    out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(flags, dev(k), dev(np.ones(n, np.float32)), out, n)
+    assert ei.value.code == (4 if bad.startswith("out_of_range") else 1)
+    k1, v1 = st.dump()
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_array_equal(v1, v0)
+    # and the store still serves requests
+    st.handle(psg.PUSH, dev(univ), dev(np.ones(len(univ), np.float32)), None, len(univ))
+    np.testing.assert_array_equal(st.dump()[1], (v0 + np.float32(1)).astype(np.float32))
+
+
+def test_dense_keyed_rejected_request_leaves_the_store_unchanged():
+    st = psg.Store(psg.DENSE, psg.F32, 100, 100000, 5000)
+    base = np.arange(5000, dtype=np.float32)
+    st.handle(psg.PUSH, None, dev(base), None, 5000, first_key=100)
+    keys = np.arange(100, 5100, dtype=np.uint64)
+    keys[-1] = 5100  # one slot past the store
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(keys), dev(np.ones(5000, np.float32)), None, 5000)
+    assert ei.value.code == 4
+    np.testing.assert_array_equal(st.dump()[1], base)
+    keys = np.arange(100, 5100, dtype=np.uint64)
+    keys[10], keys[11] = keys[11], keys[10]
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(keys), dev(np.ones(5000, np.float32)), None, 5000)
+    assert ei.value.code == 1
+    np.testing.assert_array_equal(st.dump()[1], base)
+
+
+_RA_BLOCK_CHILD = """
+import sys, numpy as np
+sys.path[:0] = {paths!r}
+import oracle, psg
+psg.set_device(0)
+rng = np.random.default_rng(77)
+univ = np.unique(rng.integers(0, 1 << 63, 200000, dtype=np.uint64))
+for dt in (psg.F32, psg.F64, psg.F16, psg.BF16):
+    st, orc = psg.Store(psg.SORTED, dt, 0, (1 << 64) - 1, 0), oracle.Store(dt)
+    for j in range(6):
+        k = np.sort(rng.choice(univ, int(rng.integers(1, len(univ))), replace=False)) if j % 2 else univ
+        v = oracle.synth(len(k), dt, 500 + j, 1, -1.0, 1.0)
+        n = len(k)
+        out = psg.DeviceBuffer(n * 8)
+        st.handle(psg.PUSH | psg.PULL, psg.DeviceBuffer.from_numpy(k), psg.DeviceBuffer.from_numpy(v), out, n)
+        exp = orc.handle(oracle.PUSH | oracle.PULL, k, v, n)
+        got = out.download({{psg.F32: np.float32, psg.F64: np.float64}}.get(dt, np.uint16), n)
+        assert np.array_equal(got, exp), (dt, j)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("block", [256, 512, 1024])
+def test_sorted_store_every_block_size(block):
+    """PSG_RA_BLOCK is read once per process: each block size of the fused
+    validate / resolve / apply kernels gets a fresh process, every dtype."""
+    import subprocess
+    import sys
+    paths = [os.path.join(os.path.dirname(HERE), "parameter-server_amd", "python"),
+             os.path.join(os.path.dirname(HERE), "oracle")]
+    env = dict(os.environ, PSG_RA_BLOCK=str(block))
+    r = subprocess.run([sys.executable, "-c", _RA_BLOCK_CHILD.format(paths=paths)], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
 def test_dense_store_resolve_slots():
     st = psg.Store(psg.DENSE, psg.F32, 100, 1000, 500)
     keys = np.array([100, 150, 599], np.uint64)
