@@ -51,11 +51,17 @@ WORKLOADS = {
     "dense": ("f32", 4, 64 << 20, 256 << 20, "configs[1]", "configs[2]"),
     "dense-f16": ("f16", 2, 1 << 30, 1 << 30, "configs[4]", "configs[4]"),
     "keyed": ("f32", 4, 10_000_000, 10_000_000, "configs[3]", "configs[3]"),
+    # configs[3] as LR_ps runs it with USE_KEY_CACHING (LRServer.h:127-142): the
+    # first request resolves the key list once, later ones name it by hash and
+    # run on the cached slots (psg_store_handle_slots)
+    "keyed-cached": ("f32", 4, 10_000_000, 10_000_000, "configs[3] (key caching)", "configs[3] (key caching)"),
 }
 # algorithmic HBM bytes per key of one keyed Push on the SORTED store:
 # request key 8 + store key 8 (resolve) + value 4 + store value read/write 8
 # (the resolve is fused with the apply: no slot array goes to HBM and back)
 KEYED_PUSH_BYTES = 28
+# ... and with a cached slot list: slot 4 + value 4 + store value read/write 8
+CACHED_PUSH_BYTES = 16
 # pushes outside warmup + steps that a run may make (calibration, verification)
 EXTRA_PUSH_BOUND = 64
 
@@ -64,13 +70,14 @@ class GpuBackend:
     """The product path: psg C-ABI (HIP kernels + RCCL)."""
 
     def __init__(self, rank: int, world: int, local_rank: int, group=None, dtype="f32",
-                 keyed=False):
+                 keyed=False, cached=False):
         import psg
         self.p = psg
         self.rank, self.world, self.group = rank, world, group
         self.dt = {"f32": psg.F32, "f16": psg.F16}[dtype]
         self.vb = {"f32": 4, "f16": 2}[dtype]
-        self.keyed = keyed
+        self.keyed = keyed or cached
+        self.cached = cached
         # PSG_BENCH_SHARE_GPU=1 (testing only): ranks share the visible GPUs
         # round-robin, and RCCL — which refuses two ranks on one GPU — is not
         # used, so the xGMI exchange path of N > 1 can run on a 1-GPU box.
@@ -105,6 +112,14 @@ class GpuBackend:
         self.vals = p.DeviceBuffer(L * self.vb)
         self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self.hi(), self.stream)
         self.out = p.DeviceBuffer(L * self.vb)
+        if self.cached:
+            if self.world > 1:
+                raise SystemExit("keyed-cached runs at N = 1 (one server)")
+            # the first request of the key list: resolve it once, inserting the
+            # keys (value 0, like the first Push's operator[]); later requests
+            # run on the cached slots
+            self.slots = p.DeviceBuffer(L * 4)
+            self.store.resolve(self.keys, L, self.slots, insert=True, stream=self.stream)
         if self.world > 1:
             if not self.share_gpu:
                 uid = self.group.broadcast(p.comm_id() if self.rank == 0 else None)
@@ -178,7 +193,9 @@ class GpuBackend:
             self.stream.sync()
             self.node_barrier.wait()
             return
-        if self.keyed:
+        if self.cached:
+            self.store.handle_slots(self.p.PUSH, self.slots, self.vals, None, self.L, stream=self.stream)
+        elif self.keyed:
             # one server: the slice is the whole request (KVWorker's DefaultSlicer
             # skips the kernel for a single range; the store's range check covers it)
             if self.comm is None:
@@ -197,7 +214,9 @@ class GpuBackend:
             self.stream.sync()
             self.node_barrier.wait()
             return
-        if self.keyed:
+        if self.cached:
+            self.store.handle_slots(self.p.PULL, self.slots, None, self.out, self.L, stream=self.stream)
+        elif self.keyed:
             if self.comm is None:
                 self.store.handle(self.p.PULL, self.keys, None, self.out, self.L, stream=self.stream)
             else:
@@ -505,7 +524,7 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         "data": "synthetic (integer-valued floats, seed 7+rank, generated in HBM)",
         "config": {
             "workload": (f"{cfg}: "
-                         + (("keyed (10 M sorted uint64 keys, SORTED store), " if wl == "keyed" else "dense, ")
+                         + (("keyed (10 M sorted uint64 keys, SORTED store), " if wl.startswith("keyed") else "dense, ")
                             + ("1 server + 1 worker, Push then Pull" if world == 1 else
                                f"ns=nw={world}, BSP Push/Pull (see exchange)"))),
             "keys_per_worker": L,
@@ -535,10 +554,16 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
             res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
         if getattr(backend, "share_gpu", False):
             res["config"]["shared_gpu_test_mode"] = True
-    if world == 1 and getattr(backend, "keyed", False):
+    if world == 1 and getattr(backend, "cached", False):
+        res["roofline"] = roofline(CACHED_PUSH_BYTES * L, push_ms, args,
+                                   "cached-slot Push: k_slots_vec (store[slot] += val, slots "
+                                   "from the one resolve of the key list)", vb)
+        res["pull_roofline_frac"] = round(12 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    elif world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
-                                   "SORTED-store Push: k_tile_windows + k_resolve_apply "
-                                   "(one host sync; one server, so no slicer pass)", vb)
+                                   "SORTED-store Push: k_validate_windows + k_resolve_apply "
+                                   "(whole-request validation before any write; one host sync; "
+                                   "one server, so no slicer pass)", vb)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
                                    "k_dense_vec<PUSH> (store += vals)", vb)
@@ -686,7 +711,8 @@ def main(argv=None) -> None:
     if world > 1:
         from psg_group import SocketGroup
         group = SocketGroup(rank, world)
-    backend = GpuBackend(rank, world, local_rank, group, dtype, keyed=args.workload == "keyed")
+    backend = GpuBackend(rank, world, local_rank, group, dtype, keyed=args.workload == "keyed",
+                         cached=args.workload == "keyed-cached")
     res = run(backend, args, rank, world, group)
     if res is not None:
         print(json.dumps(res), flush=True)

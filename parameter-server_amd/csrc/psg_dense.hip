@@ -124,6 +124,71 @@ __global__ __launch_bounds__(256) void k_slots(typename Elem<DT>::T* __restrict_
   }
 }
 
+// The same for 4-byte values, four slots per lane: 16-B loads of the slots and
+// the request values, 16-B stores of the replies, and — when the four slots
+// are consecutive and 16-B aligned (a cached slot list that covers a stretch
+// of the store, the steady state of LR key caching) — one 16-B load and store
+// of the store values instead of four.  U groups of four in flight per lane.
+// Bytes per key: slot 4 + value 4 + store 4 read / 4 written (+ reply 4).
+// Slots must be unique within a request (psg_store_resolve's lists are).
+template <int DT, int OP, int U>
+__global__ __launch_bounds__(256) void k_slots_vec(typename Elem<DT>::T* __restrict__ store,
+                                                   const u32x4* __restrict__ slots,
+                                                   const u32x4* __restrict__ vals,
+                                                   u32x4* __restrict__ out, uint64_t nq) {
+  using T = typename Elem<DT>::T;
+  static_assert(sizeof(T) == 4, "4-byte values");
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock * U;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * kBlock * U + threadIdx.x; j0 < nq; j0 += stride) {
+    u32x4 sl[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t j = j0 + (uint64_t)u * kBlock;
+      if (j < nq) {
+        sl[u] = __builtin_nontemporal_load(slots + j);
+        if constexpr ((OP & PSG_PUSH) != 0) v[u] = __builtin_nontemporal_load(vals + j);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t j = j0 + (uint64_t)u * kBlock;
+      if (j >= nq) continue;
+      // whole-vector bit casts only: __builtin_bit_cast of a vector ELEMENT
+      // (x[k]) reads element 0 with this compiler, so elements are taken from
+      // vectors of T
+      typedef T t4 __attribute__((ext_vector_type(4)));
+      t4 o = {(T)0.0f, (T)0.0f, (T)0.0f, (T)0.0f};
+      t4 vv = {(T)0.0f, (T)0.0f, (T)0.0f, (T)0.0f};
+      if constexpr ((OP & PSG_PUSH) != 0) vv = __builtin_bit_cast(t4, v[u]);
+      const uint32_t p0 = sl[u][0];
+      if (p0 != 0xffffffffu && sl[u][1] == p0 + 1 && sl[u][2] == p0 + 2 && sl[u][3] == p0 + 3 && (p0 & 3) == 0) {
+        u32x4* sp = reinterpret_cast<u32x4*>(store + p0);
+        t4 x = __builtin_bit_cast(t4, *sp);
+        if constexpr ((OP & PSG_PUSH) != 0) {
+          x = x + vv;
+          *sp = __builtin_bit_cast(u32x4, x);
+        }
+        o = x;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t p = sl[u][k];
+          T y = (T)0.0f;
+          if (p != 0xffffffffu) {
+            y = store[p];
+            if constexpr ((OP & PSG_PUSH) != 0) {
+              y = y + vv[k];
+              store[p] = y;
+            }
+          }
+          o[k] = y;
+        }
+      }
+      if constexpr ((OP & PSG_PULL) != 0) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), out + j);
+    }
+  }
+}
+
 // ---- tuning knobs ------------------------------------------------------------
 // Defaults from the MI355X sweep (profiles/r1_sweep_dense_{64M,256M}.json):
 // 2 vectors per stream in flight per lane, 2 blocks of 256 per CU (512 blocks
@@ -275,6 +340,35 @@ template <int DT>
 static int run_slots(int op, void* store, const uint32_t* slots, const void* vals, void* out,
                      uint64_t n, hipStream_t s) {
   using T = typename Elem<DT>::T;
+  if constexpr (sizeof(T) == 4) {
+    const bool need_vals = (op & PSG_PUSH) != 0, need_out = (op & PSG_PULL) != 0;
+    const uint64_t nq = (aligned16(slots) && (!need_vals || aligned16(vals)) && (!need_out || aligned16(out)))
+                            ? n / 4 : 0;
+    if (nq) {
+      constexpr int U = 2;
+      const unsigned g = stream_grid(nq, (uint64_t)kBlock * U, 4);
+      switch (op) {
+        case PSG_PUSH:
+          k_slots_vec<DT, PSG_PUSH, U><<<g, kBlock, 0, s>>>((T*)store, (const u32x4*)slots, (const u32x4*)vals,
+                                                            (u32x4*)out, nq);
+          break;
+        case PSG_PULL:
+          k_slots_vec<DT, PSG_PULL, U><<<g, kBlock, 0, s>>>((T*)store, (const u32x4*)slots, (const u32x4*)vals,
+                                                            (u32x4*)out, nq);
+          break;
+        default:
+          k_slots_vec<DT, PSG_PUSH | PSG_PULL, U><<<g, kBlock, 0, s>>>(
+              (T*)store, (const u32x4*)slots, (const u32x4*)vals, (u32x4*)out, nq);
+      }
+      PSG_HIP(hipGetLastError());
+      const uint64_t done = nq * 4;
+      if (done == n) return PSG_OK;
+      slots += done;
+      vals = need_vals ? (const void*)((const T*)vals + done) : nullptr;
+      out = need_out ? (void*)((T*)out + done) : nullptr;
+      n -= done;
+    }
+  }
   unsigned g = stream_grid(n, kBlock, 8);
   switch (op) {
     case PSG_PUSH:

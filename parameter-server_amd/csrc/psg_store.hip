@@ -191,54 +191,61 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 }
 
 // Pass 1 of a SORTED request: validate the whole request and find each
-// tile's window of K.  One block per request tile of NT * 4 keys (the tile of
-// k_resolve_apply): every lane loads its 4 keys (16-B loads) and the key
-// before them, and checks strict ascent and the shard's range [kb, ke); wave 0
-// finds wlo[tile] = lower_bound(K, q[t0]) and, in the last tile, wave 1 finds
-// wlo[ntiles] = lower_bound(K, q[n - 1]) + 1.  An invalid request sets
-// *reject = seq, which k_resolve_apply checks before it writes anything, and
-// raises F_UNSORTED / F_RANGE for the host.  Bytes: the request keys once
-// (8 B / key; k_resolve_apply's re-read of them right after is served mostly
-// by the Infinity Cache) plus ~4 scattered 512-B probes per tile end.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_validate_windows(const uint64_t* __restrict__ q, uint64_t n,
-                                                         const uint64_t* __restrict__ K, uint64_t S,
-                                                         uint64_t* __restrict__ wlo, uint64_t kb,
-                                                         uint64_t ke, int* __restrict__ reject, int seq,
-                                                         int* __restrict__ flags, int vec) {
-  constexpr uint64_t tileN = (uint64_t)NT * kPerLane;
-  int range = 0, unsorted = 0;
+// tile's window of K, as two kinds of 256-thread blocks of one launch:
+//   blocks [0, nsearch)  one wave per window bound: wlo[t] = lower_bound(K,
+//                        q[t * tileN]) for t < ntiles, wlo[ntiles] =
+//                        lower_bound(K, q[n - 1]) + 1 (a 64-ary search, ~4
+//                        dependent scattered probes of 512 B);
+//   the other blocks     stream the request keys (1024 per block, 4 per lane,
+//                        16-B loads) and check strict ascent — against the key
+//                        before each lane's four — and the shard's range [kb, ke).
+// The search blocks come first in dispatch order, so their latency runs under
+// the key stream.  An invalid request sets *reject = seq, which
+// k_resolve_apply checks before it writes anything, and raises F_UNSORTED /
+// F_RANGE for the host.  Bytes: the request keys once (8 B / key, default
+// cache policy so k_resolve_apply's re-read right after can hit the Infinity
+// Cache) plus the probes.
+__global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __restrict__ q, uint64_t n,
+                                                          const uint64_t* __restrict__ K, uint64_t S,
+                                                          uint64_t* __restrict__ wlo, uint64_t tileN,
+                                                          unsigned nsearch, uint64_t kb, uint64_t ke,
+                                                          int* __restrict__ reject, int seq,
+                                                          int* __restrict__ flags, int vec) {
   const uint64_t ntiles = (n + tileN - 1) / tileN;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t t0 = tile * tileN;
-    const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
-    const int wave = threadIdx.x >> 6;
-    if (wave == 0) {
-      const uint64_t r = lower_bound_wave(K, S, q[t0]);
-      if ((threadIdx.x & 63) == 0) wlo[tile] = r;
-    } else if (wave == 1 && tile + 1 == ntiles) {
-      const uint64_t h = lower_bound_wave(K, S, q[n - 1]);
-      if ((threadIdx.x & 63) == 0) wlo[ntiles] = h < S ? h + 1 : S;
-    }
-    const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
-    if (i0 < t1) {
-      uint64_t key[kPerLane];
-      if (i0 + kPerLane <= t1 && vec) {
-        const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0));
-        const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0 + 2));
-        key[0] = a[0];
-        key[1] = a[1];
-        key[2] = b[0];
-        key[3] = b[1];
+  if (blockIdx.x < nsearch) {
+    const uint64_t waves = (uint64_t)nsearch * (kBlock / 64);
+    for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t <= ntiles; t += waves) {
+      if (t < ntiles) {
+        const uint64_t r = lower_bound_wave(K, S, q[t * tileN]);
+        if ((threadIdx.x & 63) == 0) wlo[t] = r;
       } else {
-#pragma unroll
-        for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : ~0ull;
+        const uint64_t h = lower_bound_wave(K, S, q[n - 1]);
+        if ((threadIdx.x & 63) == 0) wlo[t] = h < S ? h + 1 : S;
       }
-      uint64_t prev = i0 > 0 ? q[i0 - 1] : 0;
-      bool first = i0 == 0;
+    }
+    return;
+  }
+  int range = 0, unsorted = 0;
+  const uint64_t nvb = (uint64_t)gridDim.x - nsearch;
+  for (uint64_t i0 = ((uint64_t)(blockIdx.x - nsearch) * kBlock + threadIdx.x) * kPerLane; i0 < n;
+       i0 += nvb * kBlock * kPerLane) {
+    uint64_t key[kPerLane];
+    if (i0 + kPerLane <= n && vec) {
+      const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0);
+      const u64x2 b = *reinterpret_cast<const u64x2*>(q + i0 + 2);
+      key[0] = a[0];
+      key[1] = a[1];
+      key[2] = b[0];
+      key[3] = b[1];
+    } else {
 #pragma unroll
-      for (int k = 0; k < kPerLane; ++k) {
-        if (i0 + k >= t1) break;
+      for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < n ? q[i0 + k] : ~0ull;
+    }
+    uint64_t prev = i0 > 0 ? q[i0 - 1] : 0;
+    bool first = i0 == 0;
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      if (i0 + k < n) {
         if (key[k] < kb || key[k] >= ke) range = 1;
         if (!first && prev >= key[k]) unsorted = 1;
         prev = key[k];
@@ -246,8 +253,7 @@ __global__ __launch_bounds__(NT) void k_validate_windows(const uint64_t* __restr
       }
     }
   }
-  const bool bad = range || unsorted;
-  if (__ballot(bad) && (threadIdx.x & 63) == 0) *reject = seq;
+  if (__ballot(range || unsorted) && (threadIdx.x & 63) == 0) *reject = seq;
   raise_flag(flags, F_RANGE, range != 0);
   raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
@@ -805,17 +811,13 @@ static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, co
   const uint64_t ntiles = (n + tile - 1) / tile;
   reset_flags(s);
   const int seq = next_seq(s);
-  const int vk = aligned16(q) ? 1 : 0;
-  const unsigned g = grid_n(ntiles, 1);
-  if (nt == 1024)
-    k_validate_windows<1024><<<g, 1024, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin, s->key_end,
-                                                 s->reject_dev, seq, s->flags, vk);
-  else if (nt == 512)
-    k_validate_windows<512><<<g, 512, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin, s->key_end,
-                                               s->reject_dev, seq, s->flags, vk);
-  else
-    k_validate_windows<256><<<g, 256, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin, s->key_end,
-                                               s->reject_dev, seq, s->flags, vk);
+  // search blocks: one wave per window bound (ntiles + 1 of them); key-stream
+  // blocks: 1024 keys each, capped at the streaming grid
+  const unsigned nsearch = (unsigned)((ntiles + 1 + kBlock / 64 - 1) / (kBlock / 64));
+  const unsigned nval = grid_n(n, (uint64_t)kBlock * kPerLane);
+  k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, tile, nsearch,
+                                                       s->key_begin, s->key_end, s->reject_dev, seq, s->flags,
+                                                       aligned16(q) ? 1 : 0);
   switch (op) {
     case PSG_PUSH: launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, st); break;
     case PSG_PULL: launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, st); break;

@@ -5,7 +5,8 @@
 # (no later GPU step runs).  Outputs land in gpurun_out/.
 #   tests    the whole -m gpu suite            smoke  __graft_entry__.smoke()
 #   bench    default bench line (configs[1])   prof   rocprof kernel stats of it
-#   keyed    keyed bench line (configs[3])     proffk rocprof kernel stats of keyed
+#   keyed    keyed bench lines (configs[3]:    proffk / profkc  rocprof kernel stats of
+#            uncached and key-cached)                  keyed / keyed-cached
 #   f16      1 G f16 bench line (configs[4])   e2e    C++ API end to end, 10 M keys
 #   t:EXPR   pytest -m gpu -k EXPR             pmc:KERNEL:ARGS  PMC traffic passes
 set -u
@@ -24,10 +25,14 @@ for st in "$@"; do
     prof) rm -rf gpurun_out/prof64
           step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof64 -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/prof64.json 2>&1; echo "prof rc=$?"
           f=$(find gpurun_out/prof64 -name "*kernel_stats.csv" | head -1); cut -c1-200 "$f" | head -12 ;;
-    keyed) step 300 python3 bench.py --workload keyed --no-cpu-baseline > gpurun_out/bench_keyed.json 2> gpurun_out/bench_keyed.err; echo "keyed rc=$?"; cat gpurun_out/bench_keyed.json; tail -3 gpurun_out/bench_keyed.err ;;
+    keyed) step 300 python3 bench.py --workload keyed --no-cpu-baseline > gpurun_out/bench_keyed.json 2> gpurun_out/bench_keyed.err; echo "keyed rc=$?"; cat gpurun_out/bench_keyed.json; tail -3 gpurun_out/bench_keyed.err
+           step 300 python3 bench.py --workload keyed-cached --no-cpu-baseline > gpurun_out/bench_keyed_cached.json 2> gpurun_out/bench_keyed_cached.err; echo "keyed-cached rc=$?"; cat gpurun_out/bench_keyed_cached.json; tail -3 gpurun_out/bench_keyed_cached.err ;;
     proffk) rm -rf gpurun_out/prof_keyed
           step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_keyed -o run --output-format csv -- python3 bench.py --workload keyed --no-cpu-baseline --steps 20 > gpurun_out/prof_keyed.json 2>&1; echo "proffk rc=$?"
           f=$(find gpurun_out/prof_keyed -name "*kernel_stats.csv" | head -1); cut -c1-200 "$f" | head -12 ;;
+    profkc) rm -rf gpurun_out/prof_keyed_cached
+          step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_keyed_cached -o run --output-format csv -- python3 bench.py --workload keyed-cached --no-cpu-baseline --steps 20 > gpurun_out/prof_keyed_cached.json 2>&1; echo "profkc rc=$?"
+          f=$(find gpurun_out/prof_keyed_cached -name "*kernel_stats.csv" | head -1); cut -c1-160 "$f" | head -8 ;;
     f16) step 300 python3 bench.py --workload dense-f16 --no-cpu-baseline > gpurun_out/bench_f16.json 2> gpurun_out/bench_f16.err; echo "f16 rc=$?"; cat gpurun_out/bench_f16.json ;;
     e2e) step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 10000000 20 > gpurun_out/e2e_threads_10M.log 2>&1; echo "e2e threads rc=$?"; head -3 gpurun_out/e2e_threads_10M.log
          step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 -procs 10000000 20 > gpurun_out/e2e_procs_10M.log 2>&1; echo "e2e procs rc=$?"; head -3 gpurun_out/e2e_procs_10M.log ;;
