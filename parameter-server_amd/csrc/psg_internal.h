@@ -147,6 +147,7 @@ struct psg_store {
   // store-writing kernel of that request reads it first and writes nothing.
   int* reject_dev;
   int seq;           // request sequence number (never 0 after the first request)
+  uint32_t done_seq; // completion words the stream has been asked to write
 };
 
 struct psg_adam {

@@ -25,6 +25,8 @@
 //   unchanged: the validation pass raises a device word that every
 //   store-writing kernel of the request checks first.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -40,6 +42,9 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // atomics), so a request needs no flag reset launch and no flag copy: the
 // host zeroes them before the launch and reads them after the stream sync.
 enum { F_MISSING = 0, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
+// the host-memory word after the flags that the stream's completion write
+// targets (read_flags); never zeroed by reset_flags
+constexpr int kDoneWord = F_NFLAGS;
 
 __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
   if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
@@ -692,8 +697,41 @@ static int run_fixup(psg_store* s, int op, const void* vals, void* out, uint64_t
   return PSG_OK;
 }
 
+// Wait for the request's kernels, then the host may read flags_host (the
+// kernels wrote it directly).  Rather than hipStreamSynchronize, the stream
+// itself writes a completion word into pinned host memory once the kernels
+// are done (hipStreamWriteValue32) and this thread spins on it: the kernels'
+// host-memory flag stores are released at kernel end, before that write.  A
+// request whose word does not appear within 2 ms (a long request, or a fault)
+// falls back to hipStreamSynchronize, which also reports any error.
+// PSG_SYNC_POLL=0 always takes hipStreamSynchronize (A/B).
+static bool sync_poll() {
+  static const bool on = [] {
+    const char* e = getenv("PSG_SYNC_POLL");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static int read_flags(psg_store* s, hipStream_t st) {
-  PSG_HIP(hipStreamSynchronize(st));  // the kernels wrote flags_host directly
+  if (sync_poll()) {
+    const uint32_t want = ++s->done_seq;
+    if (hipStreamWriteValue32(st, s->flags + kDoneWord, want, 0) == hipSuccess) {
+      volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(s->flags_host + kDoneWord);
+      auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t spin = 0;; ++spin) {
+        if (*w == want) {
+          std::atomic_thread_fence(std::memory_order_acquire);
+          return PSG_OK;
+        }
+        if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        __builtin_ia32_pause();
+      }
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  PSG_HIP(hipStreamSynchronize(st));
   return PSG_OK;
 }
 
@@ -946,12 +984,12 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
     return rc;
   };
   hipError_t e;
-  if ((e = hipHostMalloc(&s->flags_host, F_NFLAGS * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) !=
+  if ((e = hipHostMalloc(&s->flags_host, (F_NFLAGS + 1) * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) !=
       hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc(flags)", __FILE__, __LINE__));
   if ((e = hipHostGetDevicePointer((void**)&s->flags, s->flags_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(flags)", __FILE__, __LINE__));
-  memset(s->flags_host, 0, F_NFLAGS * sizeof(int));
+  memset(s->flags_host, 0, (F_NFLAGS + 1) * sizeof(int));
   if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
       (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(reject word)", __FILE__, __LINE__));
