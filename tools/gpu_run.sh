@@ -8,7 +8,8 @@
 #   keyed    keyed bench lines (configs[3]:    proffk / profkc  rocprof kernel stats of
 #            uncached and key-cached)                  keyed / keyed-cached
 #   f16      1 G f16 bench line (configs[4])   e2e    C++ API end to end, 10 M keys
-#   t:EXPR   pytest -m gpu -k EXPR             pmc:KERNEL:ARGS  PMC traffic passes
+#   t:EXPR   pytest -m gpu -k EXPR             pmck / pmckc  PMC traffic of the keyed /
+#                                                      key-cached Push (two passes each)
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -33,6 +34,13 @@ for st in "$@"; do
     profkc) rm -rf gpurun_out/prof_keyed_cached
           step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_keyed_cached -o run --output-format csv -- python3 bench.py --workload keyed-cached --no-cpu-baseline --steps 20 > gpurun_out/prof_keyed_cached.json 2>&1; echo "profkc rc=$?"
           f=$(find gpurun_out/prof_keyed_cached -name "*kernel_stats.csv" | head -1); cut -c1-160 "$f" | head -8 ;;
+    pmck|pmckc)
+          if [ "$st" = pmck ]; then wl=keyed; ks="k_validate_windows|k_resolve_apply<0, 1,"; per=28; out=pmc_keyed_push_traffic.json
+          else wl=keyed-cached; ks="k_slots_vec<0, 1,"; per=16; out=pmc_keyed_cached_push_traffic.json; fi
+          rm -rf gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st
+          step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
+          step 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_w_$st.log 2>&1; echo "$st write rc=$?"
+          python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" 10000000 gpurun_out/$out $per ;;
     f16) step 300 python3 bench.py --workload dense-f16 --no-cpu-baseline > gpurun_out/bench_f16.json 2> gpurun_out/bench_f16.err; echo "f16 rc=$?"; cat gpurun_out/bench_f16.json ;;
     e2e) step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 10000000 20 > gpurun_out/e2e_threads_10M.log 2>&1; echo "e2e threads rc=$?"; head -3 gpurun_out/e2e_threads_10M.log
          step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 -procs 10000000 20 > gpurun_out/e2e_procs_10M.log 2>&1; echo "e2e procs rc=$?"; head -3 gpurun_out/e2e_procs_10M.log ;;
