@@ -17,11 +17,12 @@
 #if defined(__GLIBCXX__) && defined(_GLIBCXX_RELEASE) && _GLIBCXX_RELEASE < 13 && __cplusplus >= 202002L
 // C++20 streams std::chrono::duration (count + unit suffix); libstdc++ gained
 // that operator in release 13.  tests/LR_ps.cpp:88 needs it, so older
-// libstdc++ gets the same output format here.
-namespace std {
-namespace chrono {
+// libstdc++ gets the same output format here — declared in the GLOBAL
+// namespace (adding it to namespace std would be undefined behaviour): the
+// harness's expression is in the global namespace, where ordinary lookup
+// finds it.
 template <class Rep, class Period>
-std::ostream& operator<<(std::ostream& os, const duration<Rep, Period>& d) {
+std::ostream& operator<<(std::ostream& os, const std::chrono::duration<Rep, Period>& d) {
   os << d.count();
   if constexpr (std::is_same_v<Period, std::nano>) os << "ns";
   else if constexpr (std::is_same_v<Period, std::micro>) os << "\xC2\xB5s";
@@ -32,8 +33,6 @@ std::ostream& operator<<(std::ostream& os, const duration<Rep, Period>& d) {
   else os << "[" << Period::num << "/" << Period::den << "]s";
   return os;
 }
-}  // namespace chrono
-}  // namespace std
 #endif
 
 namespace ps_log {
