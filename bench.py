@@ -229,12 +229,41 @@ class GpuBackend:
 
     # -- both, pipelined over buckets (N > 1)
     def step(self):
+        if self.mode == "xgmi":
+            self._xgmi_double_buffered_step()
+            return
         self.comm.push_pull(self.store, self.vals, self.out, self.L, self.nbuckets, self.stream)
+
+    def _xgmi_double_buffered_step(self):
+        """configs[4]'s double-buffered step over xGMI: every chunk's Push is
+        queued on the main stream; the Pull of chunk c goes on a second stream
+        as soon as every rank has pushed chunk c (a node barrier per chunk), so
+        it runs while the Push of chunk c + 1 is in flight.  A last barrier
+        after the Pulls keeps the next step's Push off shards a peer still reads."""
+        p = self.p
+        if getattr(self, "stream2", None) is None:
+            self.stream2 = p.Stream()
+        unit = 16 // self.vb
+        chunk = ((self.blk + self.nbuckets - 1) // self.nbuckets + unit - 1) // unit * unit
+        bounds = [(off, min(chunk, self.blk - off)) for off in range(0, self.blk, chunk)]
+        evs = getattr(self, "_db_events", [])
+        while len(evs) < len(bounds):
+            evs.append(p.Event())
+        self._db_events = evs
+        for i, (off, cnt) in enumerate(bounds):
+            self.xgmi.push_range(self.store, self.L, off, cnt, self.stream)
+            evs[i].record(self.stream)
+        for i, (off, cnt) in enumerate(bounds):
+            evs[i].sync()
+            self.node_barrier.wait()  # every rank has pushed chunk i
+            self.xgmi.pull_range(self.store, self.out, self.L, off, cnt, self.stream2)
+        self.stream2.sync()
+        self.node_barrier.wait()
 
     def _set_mode(self, cand):
         mode, nb = cand
         self.mode, self.nbuckets = mode, nb
-        self.fused = mode == "rccl" and nb > 1
+        self.fused = nb > 1
 
     def calibrate(self, iters=3):
         """Pick the exchange for this node by timing each candidate a few times
@@ -246,7 +275,13 @@ class GpuBackend:
             return
         cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
         if self.xgmi is not None:
-            cands.append(("xgmi", 0))
+            cands += [("xgmi", 0), ("xgmi", 2), ("xgmi", 4)]
+        forced = os.environ.get("PSG_BENCH_EXCHANGE")  # testing: e.g. "xgmi/4", "rccl/1"
+        if forced:
+            m, _, nb = forced.partition("/")
+            cands = [c for c in cands if c == (m, int(nb or 0))]
+            if not cands:
+                raise SystemExit(f"PSG_BENCH_EXCHANGE={forced}: not available here")
         times = []
         for cand in cands:
             self._set_mode(cand)
@@ -262,7 +297,7 @@ class GpuBackend:
         t = self.group.allreduce_max(times)
         order = sorted(range(len(cands)), key=lambda i: t[i])
         self._set_mode(cands[order[0]])
-        self.calibration = {f"{m}{'' if m == 'xgmi' else '/' + str(nb)}": round(x, 4)
+        self.calibration = {f"{m}{'' if nb == 0 else '/' + str(nb)}": round(x, 4)
                             for (m, nb), x in zip(cands, t)}
         self.pushes_in_calibration = len(cands) * (iters + 1)
         if self.mode == "xgmi":
@@ -555,7 +590,10 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                                            "+ an oracle replay at the start of every block",
                                 "elements_per_rank": L}
     if world > 1 and hasattr(backend, "nbuckets"):
-        if getattr(backend, "mode", "rccl") == "xgmi":
+        if getattr(backend, "mode", "rccl") == "xgmi" and fused:
+            res["config"]["exchange"] = ("xGMI kernels double-buffered over %d chunks: chunk c's Pull on a "
+                                         "second HIP stream while chunk c+1's Push runs" % backend.nbuckets)
+        elif getattr(backend, "mode", "rccl") == "xgmi":
             res["config"]["exchange"] = "one-shot xGMI kernels (psg_xgmi push/pull, peers via hipIpc)"
         elif getattr(backend, "keyed", False):
             res["config"]["exchange"] = "RCCL grouped reduce / broadcast of the key-range segments"

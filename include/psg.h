@@ -300,6 +300,15 @@ int psg_xgmi_destroy(psg_xgmi* x);
 int psg_xgmi_push(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream);
 /* out[w * blk ...] = shard of rank w, for every w */
 int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream);
+/* The same on elements [off, off + cnt) of every block (16-B multiples): the
+ * chunks of a double-buffered step, where the Pull of chunk c (one stream)
+ * runs while the Push of chunk c + 1 (another stream) is in flight —
+ * configs[4]'s "Push/Pull double-buffered on HIP streams".  The caller orders
+ * the ranks per chunk (psg_node_barrier after every rank's Push of chunk c). */
+int psg_xgmi_push_range(psg_xgmi* x, psg_store* shard, uint64_t n_total, uint64_t off,
+                        uint64_t cnt, psg_stream stream);
+int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total,
+                        uint64_t off, uint64_t cnt, psg_stream stream);
 /* Host barrier of the ranks of one node over a POSIX shared-memory page. */
 int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier** out);
 int psg_node_barrier_wait(psg_barrier* b, double timeout_s);

@@ -58,11 +58,12 @@ __global__ __launch_bounds__(256) void k_xgmi_push(u32x4* __restrict__ store, Pe
   }
 }
 
-// out[w*blk ...] = shard_w (16-B vectors); blockIdx.y = w.
-__global__ __launch_bounds__(256) void k_xgmi_pull(u32x4* __restrict__ out, Peers shard, uint64_t nvec) {
+// out[w*ostride ...] = shard_w (16-B vectors, nvec of them); blockIdx.y = w.
+__global__ __launch_bounds__(256) void k_xgmi_pull(u32x4* __restrict__ out, Peers shard, uint64_t nvec,
+                                                   uint64_t ostride) {
   const int w = blockIdx.y;
   const u32x4* __restrict__ s = shard.p[w];
-  u32x4* __restrict__ o = out + (uint64_t)w * nvec;
+  u32x4* __restrict__ o = out + (uint64_t)w * ostride;
   for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nvec;
        j += (uint64_t)gridDim.x * kBlock)
     __builtin_nontemporal_store(s[j], o + j);
@@ -153,32 +154,42 @@ int psg_xgmi_destroy(psg_xgmi* x) {
   return PSG_OK;
 }
 
-int psg_xgmi_push(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream) {
+int psg_xgmi_push_range(psg_xgmi* x, psg_store* shard, uint64_t n_total, uint64_t off, uint64_t cnt,
+                        psg_stream stream) {
   PSG_REQUIRE(x && shard && shard->kind == PSG_STORE_DENSE, PSG_ERR_INVALID,
               "psg_xgmi_push: need a DENSE shard");
   PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_push: n_total %% nranks");
   const uint64_t blk = n_total / (uint64_t)x->nranks;
   PSG_REQUIRE(shard->capacity >= blk, PSG_ERR_RANGE, "psg_xgmi_push: shard too small");
+  PSG_REQUIRE(off <= blk && cnt <= blk - off, PSG_ERR_RANGE, "psg_xgmi_push: range [%llu, +%llu) outside the block",
+              (unsigned long long)off, (unsigned long long)cnt);
   PSG_REQUIRE(shard->vals == x->stores[x->rank], PSG_ERR_INVALID, "psg_xgmi_push: shard is not this rank's store");
   const int es = shard->esize;
-  PSG_REQUIRE((blk * es) % 16 == 0, PSG_ERR_INVALID, "psg_xgmi_push: block must be a multiple of 16 B");
-  const uint64_t nvec = blk * es / 16;
+  PSG_REQUIRE((blk * es) % 16 == 0 && (off * es) % 16 == 0 && (cnt * es) % 16 == 0, PSG_ERR_INVALID,
+              "psg_xgmi_push: block, offset and count must be multiples of 16 B");
+  const uint64_t nvec = cnt * es / 16;
   if (nvec == 0) return PSG_OK;
   Peers src;
   for (int w = 0; w < x->nranks; ++w)
-    src.p[w] = (const u32x4*)((const char*)x->vals[w] + (uint64_t)x->rank * blk * es);
+    src.p[w] = (const u32x4*)((const char*)x->vals[w] + ((uint64_t)x->rank * blk + off) * es);
+  u32x4* dst = (u32x4*)((char*)shard->vals + off * es);
   uint64_t g = (nvec + kBlock - 1) / kBlock;
   const uint64_t cap = (uint64_t)max_stream_blocks() / 4;  // 2 per CU
   if (g > cap) g = cap;
   hipStream_t st = (hipStream_t)stream;
   switch (shard->dtype) {
-    case PSG_F32: k_xgmi_push<PSG_F32><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
-    case PSG_F64: k_xgmi_push<PSG_F64><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
-    case PSG_F16: k_xgmi_push<PSG_F16><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
-    default: k_xgmi_push<PSG_BF16><<<(unsigned)g, kBlock, 0, st>>>((u32x4*)shard->vals, src, x->nranks, nvec); break;
+    case PSG_F32: k_xgmi_push<PSG_F32><<<(unsigned)g, kBlock, 0, st>>>(dst, src, x->nranks, nvec); break;
+    case PSG_F64: k_xgmi_push<PSG_F64><<<(unsigned)g, kBlock, 0, st>>>(dst, src, x->nranks, nvec); break;
+    case PSG_F16: k_xgmi_push<PSG_F16><<<(unsigned)g, kBlock, 0, st>>>(dst, src, x->nranks, nvec); break;
+    default: k_xgmi_push<PSG_BF16><<<(unsigned)g, kBlock, 0, st>>>(dst, src, x->nranks, nvec); break;
   }
   PSG_HIP(hipGetLastError());
   return PSG_OK;
+}
+
+int psg_xgmi_push(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream) {
+  PSG_REQUIRE(x && shard, PSG_ERR_INVALID, "psg_xgmi_push: null argument");
+  return psg_xgmi_push_range(x, shard, n_total, 0, n_total / (uint64_t)x->nranks, stream);
 }
 
 // LR BSP Push over xGMI: rank r reads block r of every rank's gradient vector
@@ -199,23 +210,32 @@ int psg_xgmi_lr_push(psg_xgmi* x, psg_store* weights, uint64_t n_total, float lr
   return lr_apply_sum(weights, 0, g, x->nranks, 1, blk, lr, adam, 0, iteration, (hipStream_t)stream);
 }
 
-int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream) {
+int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, uint64_t off,
+                        uint64_t cnt, psg_stream stream) {
   PSG_REQUIRE(x && shard && out, PSG_ERR_INVALID, "psg_xgmi_pull: null argument");
   PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_pull: n_total %% nranks");
   const int es = shard->esize;
   const uint64_t blk = n_total / (uint64_t)x->nranks;
-  PSG_REQUIRE((blk * es) % 16 == 0 && aligned16(out), PSG_ERR_INVALID,
-              "psg_xgmi_pull: blocks and out must be 16-B aligned");
-  const uint64_t nvec = blk * es / 16;
+  PSG_REQUIRE(off <= blk && cnt <= blk - off, PSG_ERR_RANGE, "psg_xgmi_pull: range [%llu, +%llu) outside the block",
+              (unsigned long long)off, (unsigned long long)cnt);
+  PSG_REQUIRE((blk * es) % 16 == 0 && (off * es) % 16 == 0 && (cnt * es) % 16 == 0 && aligned16(out),
+              PSG_ERR_INVALID, "psg_xgmi_pull: blocks, offset, count and out must be 16-B aligned");
+  const uint64_t nvec = cnt * es / 16;
   if (nvec == 0) return PSG_OK;
   Peers sh;
-  for (int w = 0; w < x->nranks; ++w) sh.p[w] = (const u32x4*)x->stores[w];
+  for (int w = 0; w < x->nranks; ++w) sh.p[w] = (const u32x4*)((const char*)x->stores[w] + off * es);
   uint64_t gx = (nvec + kBlock - 1) / kBlock;
   const uint64_t cap = (uint64_t)max_stream_blocks() / 4 / (uint64_t)x->nranks + 1;
   if (gx > cap) gx = cap;
-  k_xgmi_pull<<<dim3((unsigned)gx, (unsigned)x->nranks), kBlock, 0, (hipStream_t)stream>>>((u32x4*)out, sh, nvec);
+  k_xgmi_pull<<<dim3((unsigned)gx, (unsigned)x->nranks), kBlock, 0, (hipStream_t)stream>>>(
+      (u32x4*)((char*)out + off * es), sh, nvec, blk * es / 16);
   PSG_HIP(hipGetLastError());
   return PSG_OK;
+}
+
+int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream) {
+  PSG_REQUIRE(x && shard, PSG_ERR_INVALID, "psg_xgmi_pull: null argument");
+  return psg_xgmi_pull_range(x, shard, out, n_total, 0, n_total / (uint64_t)x->nranks, stream);
 }
 
 // ---- node barrier: a sense-counting barrier in a POSIX shared-memory page --

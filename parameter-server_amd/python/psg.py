@@ -48,7 +48,8 @@ EXPORTS = [
     "psg_adam_create", "psg_adam_destroy", "psg_lr_apply", "psg_lr_apply_sum",
     "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
-    "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_node_barrier_create",
+    "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_xgmi_push_range",
+    "psg_xgmi_pull_range", "psg_node_barrier_create",
     "psg_node_barrier_wait", "psg_node_barrier_destroy",
 ]
 
@@ -132,6 +133,8 @@ def lib() -> C.CDLL:
             "psg_xgmi_create": ([i32, i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)], i32),
             "psg_xgmi_destroy": ([vp], i32), "psg_xgmi_push": ([vp, vp, u64, vp], i32),
             "psg_xgmi_pull": ([vp, vp, vp, u64, vp], i32),
+            "psg_xgmi_push_range": ([vp, vp, u64, u64, u64, vp], i32),
+            "psg_xgmi_pull_range": ([vp, vp, vp, u64, u64, u64, vp], i32),
             "psg_node_barrier_create": ([C.c_char_p, i32, i32, C.POINTER(vp)], i32),
             "psg_node_barrier_wait": ([vp, f64], i32), "psg_node_barrier_destroy": ([vp], i32),
         }
@@ -482,6 +485,12 @@ class Xgmi:
 
     def pull(self, shard: Store, out, n_total: int, stream=None) -> None:
         _call("psg_xgmi_pull", self.h, shard.h, _ptr(out), n_total, _s(stream))
+
+    def push_range(self, shard: Store, n_total: int, off: int, cnt: int, stream=None) -> None:
+        _call("psg_xgmi_push_range", self.h, shard.h, n_total, off, cnt, _s(stream))
+
+    def pull_range(self, shard: Store, out, n_total: int, off: int, cnt: int, stream=None) -> None:
+        _call("psg_xgmi_pull_range", self.h, shard.h, _ptr(out), n_total, off, cnt, _s(stream))
 
     def lr_push(self, weights: Store, n_total: int, lr: float, adam=None, iteration=0,
                 stream=None) -> None:

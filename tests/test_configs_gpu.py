@@ -105,3 +105,35 @@ def test_configs3_keyed_10m_ns4_vs_oracle():
         ok, ov = ostores[s].dump()
         order = np.argsort(ok)
         assert np.array_equal(k, ok[order]) and np.array_equal(v, ov[order])
+
+
+def _bench_shared(nranks, extra, env_extra, timeout=600):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PSG_BENCH_SHARE_GPU="1", **env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(nranks)] + extra
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+
+
+def test_configs4_n8_f16_1g_double_buffered_shared_gpu():
+    """configs[4]: 1 G fp16 values per worker, nw = ns = 8, the step
+    double-buffered on two HIP streams (chunk c's Pull while chunk c+1's Push
+    runs), every rank's whole pulled vector checked against the closed form."""
+    res = _bench_shared(8, ["--workload", "dense-f16", "--steps", "2", "--warmup", "1"],
+                        {"PSG_BENCH_EXCHANGE": "xgmi/4"})
+    assert res["parity_check"] is True and res["dtype"] == "f16", res
+    assert res["config"]["keys_per_worker"] == 1 << 30 and res["n_gpus"] == 8
+    assert "double-buffered" in res["config"]["exchange"], res["config"]
+
+
+def test_xgmi_double_buffered_ragged_chunks():
+    """3 ranks, a block of 16,004 floats in 4 chunks of 4,004 / 4,004 / 4,004 / 3,992."""
+    res = _bench_shared(3, ["--keys", str(3 * 16004), "--steps", "4", "--warmup", "2"],
+                        {"PSG_BENCH_EXCHANGE": "xgmi/4"}, timeout=300)
+    assert res["parity_check"] is True, res
+    assert "double-buffered over 4 chunks" in res["config"]["exchange"]
