@@ -122,6 +122,15 @@ int max_stream_blocks();
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Bytes to hipMalloc for an array a peer process may map (hipIpc): the HIP
+// runtime may carve allocations below 2 MiB out of a shared block, and such a
+// pointer's IPC handle cannot always be opened ("invalid device pointer"), so
+// arrays of 64 KiB and more are rounded up to whole 2 MiB pages.
+inline size_t ipc_alloc_bytes(size_t bytes) {
+  constexpr size_t kPage = 2u << 20;
+  return bytes < (64u << 10) ? bytes : (bytes + kPage - 1) / kPage * kPage;
+}
+
 // ---- store ------------------------------------------------------------------
 }  // namespace psg
 

@@ -193,7 +193,7 @@ int psg_malloc(void** dptr, size_t bytes) {
   PSG_REQUIRE(dptr, PSG_ERR_INVALID, "psg_malloc: null out");
   *dptr = nullptr;
   if (bytes == 0) return PSG_OK;
-  PSG_HIP(hipMalloc(dptr, bytes));
+  PSG_HIP(hipMalloc(dptr, ipc_alloc_bytes(bytes)));
   return PSG_OK;
 }
 int psg_free(void* dptr) {

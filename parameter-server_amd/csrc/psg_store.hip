@@ -996,7 +996,8 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
   if (kind == PSG_STORE_DENSE) {
     s->capacity = capacity;
     s->size = capacity;
-    if ((e = hipMalloc(&s->vals, capacity * es)) != hipSuccess)
+    // a DENSE shard is what peers map for the xGMI exchange (psg_xgmi_create)
+    if ((e = hipMalloc(&s->vals, ipc_alloc_bytes(capacity * es))) != hipSuccess)
       return fail(hip_fail(e, "hipMalloc(store values)", __FILE__, __LINE__));
     if ((e = hipMemset(s->vals, 0, capacity * es)) != hipSuccess)
       return fail(hip_fail(e, "hipMemset(store values)", __FILE__, __LINE__));

@@ -265,6 +265,17 @@ int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier*
                   "node barrier %s: rank 0 never created it (%s)", nm.c_str(), strerror(errno));
       usleep(1000);
     }
+    // rank 0 creates the object empty and sizes it next: mapping it before
+    // that would fault (SIGBUS) on the first access
+    struct stat sb;
+    for (int tries = 0; fstat(fd, &sb) == 0 && sb.st_size < 4096; ++tries) {
+      if (tries >= 60000) {
+        close(fd);
+        set_error("node barrier %s: never sized by rank 0", nm.c_str());
+        return PSG_ERR_COMM;
+      }
+      usleep(1000);
+    }
   }
   void* p = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);

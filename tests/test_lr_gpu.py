@@ -167,7 +167,7 @@ def _xgmi_lr_rank_body(rank, world, n, rounds, adam, name, q_in, q_out):
 
 @pytest.mark.parametrize("world,adam", [(2, True), (3, False)])
 def test_xgmi_lr_push_multiprocess(world, adam):
-    n = 3 * 64 * 1024 + 0  # divisible by 2 and 3, 16-B blocks
+    n = 3 * 64 * 16384  # divisible by 2 and 3, 16-B blocks; shards of 8-12 MB
     rounds = 3
     ctx = mp.get_context("spawn")
     q_out = ctx.Queue()
