@@ -121,6 +121,9 @@ class GpuBackend:
             self.slots = p.DeviceBuffer(L * 4)
             self.store.resolve(self.keys, L, self.slots, insert=True, stream=self.stream)
         if self.world > 1:
+            if self.keyed and self.share_gpu:
+                raise SystemExit("the keyed N > 1 exchange runs on RCCL: one GPU per rank "
+                                 "(PSG_BENCH_SHARE_GPU has no keyed path)")
             if not self.share_gpu:
                 uid = self.group.broadcast(p.comm_id() if self.rank == 0 else None)
                 self.comm = p.Comm(uid, self.world, self.rank)
