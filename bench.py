@@ -278,8 +278,16 @@ class GpuBackend:
             return
         cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
         if self.xgmi is not None:
-            cands += [("xgmi", 0), ("xgmi", 2), ("xgmi", 4)]
+            cands.append(("xgmi", 0))
+            # the double-buffered step adds a second stream per rank; with every
+            # rank on ONE GPU (test mode) that oversubscribes the hardware queues
+            # and slows every later step ~4x (measured at N = 8), so test mode
+            # times it only when forced
+            if not self.share_gpu:
+                cands += [("xgmi", 2), ("xgmi", 4)]
         forced = os.environ.get("PSG_BENCH_EXCHANGE")  # testing: e.g. "xgmi/4", "rccl/1"
+        if forced and self.xgmi is not None:
+            cands += [c for c in (("xgmi", 2), ("xgmi", 4)) if c not in cands]
         if forced:
             m, _, nb = forced.partition("/")
             cands = [c for c in cands if c == (m, int(nb or 0))]
