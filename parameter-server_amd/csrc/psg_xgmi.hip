@@ -59,14 +59,30 @@ __global__ __launch_bounds__(256) void k_xgmi_push(u32x4* __restrict__ store, Pe
 }
 
 // out[w*ostride ...] = shard_w (16-B vectors, nvec of them); blockIdx.y = w.
+// Four loads in flight per lane before the stores: a read of a peer's HBM over
+// xGMI waits microseconds, and Little's law at ~1 TB/s of ingress needs several
+// MB in flight across the chip (512 blocks x 256 lanes x 64 B = 8 MB).
+constexpr int kPullU = 4;
 __global__ __launch_bounds__(256) void k_xgmi_pull(u32x4* __restrict__ out, Peers shard, uint64_t nvec,
                                                    uint64_t ostride) {
   const int w = blockIdx.y;
   const u32x4* __restrict__ s = shard.p[w];
   u32x4* __restrict__ o = out + (uint64_t)w * ostride;
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nvec;
-       j += (uint64_t)gridDim.x * kBlock)
-    __builtin_nontemporal_store(s[j], o + j);
+  const uint64_t tile = (uint64_t)kBlock * kPullU;
+  for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec;
+       base += (uint64_t)gridDim.x * tile) {
+    u32x4 v[kPullU];
+#pragma unroll
+    for (int u = 0; u < kPullU; ++u) {
+      const uint64_t j = base + (uint64_t)u * kBlock;
+      if (j < nvec) v[u] = __builtin_nontemporal_load(s + j);
+    }
+#pragma unroll
+    for (int u = 0; u < kPullU; ++u) {
+      const uint64_t j = base + (uint64_t)u * kBlock;
+      if (j < nvec) __builtin_nontemporal_store(v[u], o + j);
+    }
+  }
 }
 
 }  // namespace psg
@@ -224,7 +240,7 @@ int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_tot
   if (nvec == 0) return PSG_OK;
   Peers sh;
   for (int w = 0; w < x->nranks; ++w) sh.p[w] = (const u32x4*)((const char*)x->stores[w] + off * es);
-  uint64_t gx = (nvec + kBlock - 1) / kBlock;
+  uint64_t gx = (nvec + (uint64_t)kBlock * kPullU - 1) / ((uint64_t)kBlock * kPullU);
   const uint64_t cap = (uint64_t)max_stream_blocks() / 4 / (uint64_t)x->nranks + 1;
   if (gx > cap) gx = cap;
   k_xgmi_pull<<<dim3((unsigned)gx, (unsigned)x->nranks), kBlock, 0, (hipStream_t)stream>>>(
