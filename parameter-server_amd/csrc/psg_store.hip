@@ -201,9 +201,9 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 //                        q[t * tileN]) for t < ntiles, wlo[ntiles] =
 //                        lower_bound(K, q[n - 1]) + 1 (a 64-ary search, ~4
 //                        dependent scattered probes of 512 B);
-//   the other blocks     stream the request keys (1024 per block, 4 per lane,
-//                        16-B loads) and check strict ascent — against the key
-//                        before each lane's four — and the shard's range [kb, ke).
+//   the other blocks     stream the request keys (8 per lane, 16-B loads) and
+//                        check strict ascent — against the key before each
+//                        lane's eight — and the shard's range [kb, ke).
 // The search blocks come first in dispatch order, so their latency runs under
 // the key stream.  An invalid request sets *reject = seq, which
 // k_resolve_apply checks before it writes anything, and raises F_UNSORTED /
@@ -230,31 +230,44 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
     }
     return;
   }
+  // 8 consecutive keys per lane (four 16-B loads in flight); the key before a
+  // lane's eight is the previous lane's last, handed over by a shuffle — only
+  // lane 0 of a wave loads it.  The loop bound is block-uniform (the shuffle
+  // needs every lane).
+  constexpr int kV = 8;
   int range = 0, unsorted = 0;
   const uint64_t nvb = (uint64_t)gridDim.x - nsearch;
-  for (uint64_t i0 = ((uint64_t)(blockIdx.x - nsearch) * kBlock + threadIdx.x) * kPerLane; i0 < n;
-       i0 += nvb * kBlock * kPerLane) {
-    uint64_t key[kPerLane];
-    if (i0 + kPerLane <= n && vec) {
-      const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0);
-      const u64x2 b = *reinterpret_cast<const u64x2*>(q + i0 + 2);
-      key[0] = a[0];
-      key[1] = a[1];
-      key[2] = b[0];
-      key[3] = b[1];
+  for (uint64_t base = (uint64_t)(blockIdx.x - nsearch) * kBlock * kV; base < n;
+       base += nvb * kBlock * kV) {
+    const uint64_t i0 = base + (uint64_t)threadIdx.x * kV;
+    uint64_t key[kV];
+    if (i0 + kV <= n && vec) {
+#pragma unroll
+      for (int h = 0; h < kV / 2; ++h) {
+        const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0 + 2 * h);
+        key[2 * h] = a[0];
+        key[2 * h + 1] = a[1];
+      }
     } else {
 #pragma unroll
-      for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < n ? q[i0 + k] : ~0ull;
+      for (int k = 0; k < kV; ++k) key[k] = i0 + k < n ? q[i0 + k] : 0;
     }
-    uint64_t prev = i0 > 0 ? q[i0 - 1] : 0;
-    bool first = i0 == 0;
+    uint64_t last = key[kV - 1];
+    if (i0 + kV > n) last = i0 < n ? key[n - 1 - i0 < kV ? n - 1 - i0 : 0] : 0;
+    const uint32_t lo = __shfl_up((uint32_t)last, 1, 64), hi = __shfl_up((uint32_t)(last >> 32), 1, 64);
+    uint64_t prev = ((uint64_t)hi << 32) | lo;
+    bool have_prev = i0 < n;
+    if ((threadIdx.x & 63) == 0) {
+      have_prev = i0 > 0 && i0 < n;
+      prev = have_prev ? q[i0 - 1] : 0;
+    }
 #pragma unroll
-    for (int k = 0; k < kPerLane; ++k) {
+    for (int k = 0; k < kV; ++k) {
       if (i0 + k < n) {
         if (key[k] < kb || key[k] >= ke) range = 1;
-        if (!first && prev >= key[k]) unsorted = 1;
+        if (have_prev && prev >= key[k]) unsorted = 1;
         prev = key[k];
-        first = false;
+        have_prev = true;
       }
     }
   }
@@ -852,7 +865,7 @@ static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, co
   // search blocks: one wave per window bound (ntiles + 1 of them); key-stream
   // blocks: 1024 keys each, capped at the streaming grid
   const unsigned nsearch = (unsigned)((ntiles + 1 + kBlock / 64 - 1) / (kBlock / 64));
-  const unsigned nval = grid_n(n, (uint64_t)kBlock * kPerLane);
+  const unsigned nval = grid_n(n, (uint64_t)kBlock * 8);
   k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, tile, nsearch,
                                                        s->key_begin, s->key_end, s->reject_dev, seq, s->flags,
                                                        aligned16(q) ? 1 : 0);
