@@ -187,6 +187,12 @@ int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots,
                            const void* vals, void* out, uint64_t n,
                            psg_stream stream);
 
+/* The hash a key list is cached under in LR key caching (the std::hash
+ * specialisation of tests/src/LRServer.h:11-29, which LRWorker.h:214-219 also
+ * computes): n XOR the XOR of splitmix64(keys[i]).  Device keys; synchronises
+ * `stream`.  Lets a server cache a list that arrives as an HBM frame. */
+int psg_key_list_hash(const uint64_t* keys, uint64_t n, uint64_t* hash_host, psg_stream stream);
+
 /* Copy the store to host memory (checkpoint, LRServer::SaveModel analogue,
  * tests/src/LRServer.h:107-115).  keys_host may be NULL for a DENSE store;
  * both arrays must hold info.size elements.  Synchronous. */

@@ -139,6 +139,30 @@ __global__ __launch_bounds__(256) void k_verify_synth_sum(const T* __restrict__ 
   }
 }
 
+// The key-list hash of LR key caching (tests/src/LRServer.h:11-29):
+// seed = n; for each key x: seed ^= splitmix64(x), whose XOR-fold is
+// order-free, so one XOR reduction over the keys computes it.  Per-block
+// partials, XOR-ed on the host.
+__global__ __launch_bounds__(256) void k_key_list_hash(const uint64_t* __restrict__ keys, uint64_t n,
+                                                       uint64_t* __restrict__ partials) {
+  uint64_t h = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    h ^= splitmix64(keys[i]);
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)h, o, 64), hi = __shfl_xor((uint32_t)(h >> 32), o, 64);
+    h ^= ((uint64_t)hi << 32) | lo;
+  }
+  __shared__ uint64_t part[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int k = 0; k < kBlock / 64; ++k) t ^= part[k];
+    partials[blockIdx.x] = t;
+  }
+}
+
 static unsigned grid_for(uint64_t n) {
   uint64_t b = (n + kBlock - 1) / kBlock;
   uint64_t cap = (uint64_t)max_stream_blocks();
@@ -332,6 +356,29 @@ int psg_checksum(const void* dptr, uint64_t nbytes, uint64_t* sum_host, psg_stre
   uint64_t h = 0;
   for (uint64_t x : host) h += x;
   *sum_host = h;
+  return PSG_OK;
+}
+
+int psg_key_list_hash(const uint64_t* keys, uint64_t n, uint64_t* hash_host, psg_stream stream) {
+  PSG_REQUIRE(hash_host, PSG_ERR_INVALID, "psg_key_list_hash: null out");
+  *hash_host = n;
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(keys, PSG_ERR_INVALID, "psg_key_list_hash: null keys");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = grid_for(n);
+  uint64_t* part = nullptr;
+  PSG_HIP(hipMalloc((void**)&part, (size_t)g * sizeof(uint64_t)));
+  std::vector<uint64_t> host(g);
+  k_key_list_hash<<<g, kBlock, 0, s>>>(keys, n, part);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(host.data(), part, (size_t)g * sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(part);
+  if (e != hipSuccess) return hip_fail(e, "psg_key_list_hash", __FILE__, __LINE__);
+  uint64_t h = n;
+  for (uint64_t x : host) h ^= x;
+  *hash_host = h;
   return PSG_OK;
 }
 

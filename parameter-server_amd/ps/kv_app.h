@@ -88,6 +88,20 @@ SVector<T> ToDeviceAsync(const SVector<T>& v, int dev) {
                 "psg_memcpy H2D");
   return d;
 }
+// The key-list hash of LR key caching: the std::hash<ps::SVector<uint64_t>>
+// specialisation of tests/src/LRServer.h:11-29, which the reference worker
+// also uses (LRWorker.h:214-219), restated so a server finds the list a
+// worker names.  psg_key_list_hash computes the same on device keys.
+inline uint64_t KeyListHash(const Key* keys, size_t n) {
+  uint64_t seed = n;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t x = keys[i] + 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    seed ^= x ^ x >> 31;
+  }
+  return seed;
+}
 }  // namespace detail
 
 template <typename Value>
@@ -271,22 +285,40 @@ class KVServer : public SimpleApp {
 
 /* The default handle (KVApp.h:433-458): `store[key] += val` for a push,
  * `res.vals[i] = store[key]` (post-update) for a pull, absent keys inserted
- * with 0 — with the store in HBM (psg_store, SORTED) and the loop as one HIP
- * kernel per request.  One value per key (the reference's CHECK at :441). */
+ * with 0 — with the store in HBM (psg_store, SORTED) and the loop as HIP
+ * kernels per request.  One value per key (the reference's CHECK at :441).
+ *
+ * KVServerDefaultHandle<V>(true) also serves the key-cache protocol of the
+ * reference's LR server (LRServer.h:127-142) on this store: a request with
+ * more than one key is handled as usual and its key list is cached under its
+ * hash (detail::KeyListHash / psg_key_list_hash), resolved once to store
+ * slots; a request with ONE key names a cached list by that hash and runs on
+ * the cached slots (psg_store_handle_slots: 16 B / key for a Push instead of
+ * a validation pass plus the resolve).  The slots are re-resolved after the
+ * store inserts keys.  As in the reference, a one-key request is then always
+ * read as a hash, and every list should go to one server (LR_ps runs ns = 1). */
 template <typename Value>
 struct KVServerDefaultHandle {
+  struct Cached {
+    SVector<Key> keys;        // the list (HBM), kept for a re-resolve
+    SVector<uint32_t> slots;  // its store slots (HBM)
+    uint64_t store_size = 0;  // the store's size when resolved (an insert moves slots)
+  };
   struct State {
     psg_store* store = nullptr;
+    bool key_cache = false;
+    std::unordered_map<uint64_t, Cached> cache;
     ~State() {
       if (store) psg_store_destroy(store);
     }
   };
   std::shared_ptr<State> state = std::make_shared<State>();
 
+  explicit KVServerDefaultHandle(bool use_key_cache = false) { state->key_cache = use_key_cache; }
+
   void operator()(const KVMeta& req_meta, const KVPairs<Value>& req_data, KVServer<Value>* server) {
-    const size_t n = req_data.keys.size();
+    size_t n = req_data.keys.size();
     KVPairs<Value> res;
-    if (req_meta.push) CHECK_EQ(n, req_data.vals.size());
     const int dev = PostOffice::Get()->device();
     CHECK_GE(dev, 0) << "KVServerDefaultHandle: the value store lives in HBM and this node has no GPU";
     constexpr int dt = device::DType<Value>();
@@ -295,16 +327,37 @@ struct KVServerDefaultHandle {
       device::Check(psg_store_create(PSG_STORE_SORTED, dt, 0, kMaxKey, 0, &state->store), "psg_store_create");
     const bool on_dev = req_data.keys.on_device();
     const int flags = (req_meta.push ? PSG_PUSH : 0) | (req_meta.pull ? PSG_PULL : 0);
+    psg_stream s = device::ThreadStream();
     SVector<Value> dout;
-    if (n && flags) {
+    if (state->key_cache && n == 1 && flags) {
+      // a cached list named by its hash (LRServer.h:129-135)
+      Key h = 0;
+      if (on_dev) device::CopySync(&h, req_data.keys.data(), sizeof(Key), 1);
+      else h = req_data.keys[0];
+      auto it = state->cache.find(h);
+      CHECK(it != state->cache.end()) << "Keys don't exist with hash value: " << h;
+      Cached& c = it->second;
+      n = c.keys.size();
+      if (req_meta.push) CHECK_EQ(n, req_data.vals.size());
+      Refresh(c, s);
+      SVector<Value> dvals;
+      if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
+      if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
+      device::Check(psg_store_handle_slots(state->store, flags, c.slots.data(), dvals.data(), dout.data(), n, s),
+                    "psg_store_handle_slots");
+      device::Check(psg_stream_sync(s), "psg_stream_sync");
+    } else if (n && flags) {
+      if (req_meta.push) CHECK_EQ(n, req_data.vals.size());
       SVector<Key> dkeys = detail::ToDeviceAsync(req_data.keys, dev);
       SVector<Value> dvals;
       if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
       if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
-      psg_stream s = device::ThreadStream();
       device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
                     "psg_store_handle");
       device::Check(psg_stream_sync(s), "psg_stream_sync");
+      if (state->key_cache) Remember(dkeys, on_dev ? 0 : detail::KeyListHash(req_data.keys.data(), n), s);
+    } else if (req_meta.push) {
+      CHECK_EQ(n, req_data.vals.size());
     }
     if (req_meta.pull) {
       res.keys = req_data.keys;
@@ -314,6 +367,7 @@ struct KVServerDefaultHandle {
   }
 
   psg_store* store() const { return state->store; }
+  size_t cached_key_lists() const { return state->cache.size(); }
   /* (key, value) pairs in key order, copied to host */
   void Dump(std::vector<Key>* keys, std::vector<Value>* vals) const {
     keys->clear();
@@ -324,6 +378,36 @@ struct KVServerDefaultHandle {
     keys->resize(info.size);
     vals->resize(info.size);
     device::Check(psg_store_dump(state->store, keys->data(), vals->data()), "psg_store_dump");
+  }
+
+ private:
+  uint64_t StoreSize() const {
+    psg_store_info info;
+    device::Check(psg_store_get_info(state->store, &info), "psg_store_get_info");
+    return info.size;
+  }
+  // cache a full list under its hash (LRServer.h:136-141: the first one wins)
+  void Remember(const SVector<Key>& dkeys, uint64_t host_hash, psg_stream s) {
+    const size_t n = dkeys.size();
+    uint64_t h = host_hash;
+    if (dkeys.on_device() && host_hash == 0)
+      device::Check(psg_key_list_hash(dkeys.data(), n, &h, s), "psg_key_list_hash");
+    if (state->cache.count(h)) return;
+    Cached c;
+    c.keys = dkeys;
+    c.slots = SVector<uint32_t>::OnDevice(n, PostOffice::Get()->device());
+    device::Check(psg_store_resolve(state->store, c.keys.data(), n, 0, c.slots.data(), s), "psg_store_resolve");
+    device::Check(psg_stream_sync(s), "psg_stream_sync");
+    c.store_size = StoreSize();
+    state->cache.emplace(h, std::move(c));
+  }
+  void Refresh(Cached& c, psg_stream s) {
+    const uint64_t size = StoreSize();
+    if (size == c.store_size) return;
+    device::Check(psg_store_resolve(state->store, c.keys.data(), c.keys.size(), 0, c.slots.data(), s),
+                  "psg_store_resolve");
+    device::Check(psg_stream_sync(s), "psg_stream_sync");
+    c.store_size = size;
   }
 };
 

@@ -29,22 +29,6 @@
 
 namespace ps {
 
-namespace detail {
-// The key-list hash of LRServer.h:11-29 (the std::hash<ps::SVector<uint64_t>>
-// specialisation the reference worker also uses), restated so the server finds
-// the list a worker names.
-inline uint64_t KeyListHash(const Key* keys, size_t n) {
-  uint64_t seed = n;
-  for (size_t i = 0; i < n; ++i) {
-    uint64_t x = keys[i] + 0x9e3779b97f4a7c15ull;
-    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
-    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
-    seed ^= x ^ x >> 31;
-  }
-  return seed;
-}
-}  // namespace detail
-
 struct KVServerLRHandle {
   struct State {
     psg_store* weights = nullptr;

@@ -42,6 +42,7 @@ EXPORTS = [
     "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
     "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
+    "psg_key_list_hash",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
@@ -109,6 +110,7 @@ def lib() -> C.CDLL:
             "psg_store_resolve": ([vp, vp, u64, i32, vp, vp], i32),
             "psg_store_handle_slots": ([vp, i32, vp, vp, vp, u64, vp], i32),
             "psg_store_dump": ([vp, vp, vp], i32),
+            "psg_key_list_hash": ([vp, u64, C.POINTER(u64), vp], i32),
             "psg_server_ranges": ([i32, vp, vp], i32),
             "psg_slice": ([vp, u64, vp, u64, i32, vp, vp, vp, vp, vp], i32),
             "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
@@ -288,6 +290,13 @@ def verify_synth_sum(ptr, n: int, dtype: int, seed0: int, nseeds: int, lo: float
     _call("psg_verify_synth_sum", C.c_void_p(_ptr(ptr)), n, dtype, seed0, nseeds, offset, lo, hi,
           scale, C.byref(bad), C.byref(first), _s(stream))
     return bad.value, (None if first.value == (1 << 64) - 1 else first.value)
+
+
+def key_list_hash(keys, n: int, stream=None) -> int:
+    """psg_key_list_hash: the LR key-cache hash of a device key list."""
+    h = C.c_uint64(0)
+    _call("psg_key_list_hash", C.c_void_p(_ptr(keys)), n, C.byref(h), _s(stream))
+    return h.value
 
 
 def checksum_host(a: np.ndarray) -> int:

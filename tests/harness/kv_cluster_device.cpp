@@ -8,7 +8,11 @@
 // expectations (50 pushes -> 50 * vals, 50 push-pulls -> 100 * vals) and
 // prints one JSON line of timings per worker:
 //   {"rank":r,"n":N,"device_push_ms":..,"device_pull_ms":..,"host_push_ms":..,"host_pull_ms":..}
-// usage: kv_cluster_device [-ns S] [-nw W] [num_keys] [repeat]
+// With key_cache = 1 the server runs KVServerDefaultHandle<float>(true) and the
+// timed requests carry ONE key, the hash of the list the untimed first
+// request sent (the LR key-cache protocol, LRServer.h:127-142 / LRWorker.h:
+// 214-219); one server only, as LR_ps.
+// usage: kv_cluster_device [-ns S] [-nw W] [num_keys] [repeat] [key_cache]
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -25,9 +29,11 @@ static double ms_since(clk::time_point t0) {
 
 int main(int argc, char* argv[]) {
   Start(0, argc, argv);
+  const bool key_cache = argc > 6 && std::atoi(argv[6]) != 0;
+  if (key_cache) CHECK_EQ(NumServers(), 1) << "a hashed key list goes to one server";
   if (IsServer()) {
     auto server = new KVServer<float>(0);
-    server->SetRequestHandle(KVServerDefaultHandle<float>());
+    server->SetRequestHandle(KVServerDefaultHandle<float>(key_cache));
     RegisterExitCallback([server]() { delete server; });
   }
   if (IsWorker()) {
@@ -52,6 +58,13 @@ int main(int argc, char* argv[]) {
     auto dout = SVector<float>::OnDevice(num, dev);
     kv.Wait(kv.ZPush(dkeys, dvals));
     kv.Wait(kv.ZPull(dkeys, &dout));
+    if (key_cache) {  // from now on the list is named by its hash
+      uint64_t h = 0;
+      device::Check(psg_key_list_hash(dkeys.data(), num, &h, s), "psg_key_list_hash");
+      auto hk = SVector<Key>::OnDevice(1, dev);
+      device::CopySync(hk.data(), &h, sizeof(h), 0);
+      dkeys = hk;
+    }
     auto t0 = clk::now();
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.ZPush(dkeys, dvals));
     double dpush = ms_since(t0) / repeat;
@@ -73,6 +86,7 @@ int main(int argc, char* argv[]) {
     std::vector<float> rets;
     kv.Wait(kv.Push(hkeys, hvals));
     kv.Wait(kv.Pull(hkeys, &rets));
+    if (key_cache) hkeys = std::vector<Key>{detail::KeyListHash(hkeys.data(), hkeys.size())};
     t0 = clk::now();
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.Push(hkeys, hvals));
     double hpush = ms_since(t0) / repeat;
@@ -85,9 +99,9 @@ int main(int argc, char* argv[]) {
     for (long i = 0; i < num; ++i)
       CHECK_EQ(outs[i], hvals[i] * (2 * repeat + 1)) << "host push-pull, i=" << i;
 
-    std::printf("{\"rank\": %d, \"n\": %ld, \"servers\": %d, \"device_push_ms\": %.4f, "
+    std::printf("{\"rank\": %d, \"n\": %ld, \"servers\": %d, \"key_cache\": %d, \"device_push_ms\": %.4f, "
                 "\"device_pull_ms\": %.4f, \"host_push_ms\": %.4f, \"host_pull_ms\": %.4f}\n",
-                rank, num, NumServers(), dpush, dpull, hpush, hpull);
+                rank, num, NumServers(), (int)key_cache, dpush, dpull, hpush, hpull);
     std::fflush(stdout);
   }
   Finalize(0, true);

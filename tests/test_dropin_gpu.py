@@ -85,6 +85,21 @@ def test_lr_server_in_hbm_matches_reference_update(nw, sync, adam, cache):
     assert "matches the reference update" in r.stdout
 
 
+@pytest.mark.parametrize("nw", [1, 2])
+def test_default_handle_key_cache_end_to_end(nw):
+    """KVServerDefaultHandle<float>(true): after one full request, every request
+    names its key list by hash (LRServer.h:127-142) and runs on cached device
+    slots — device frames (hash from psg_key_list_hash) and host frames (hash
+    from detail::KeyListHash), Push, Pull and PushPull, with the harness's
+    closed-form checks."""
+    exe = os.path.join(BIN, "kv_cluster_device")
+    _need(exe)
+    r = run(exe, "-ns", 1, "-nw", nw, 200000, 5, 1)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == nw and all(l["key_cache"] == 1 for l in lines)
+
+
 @pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
 def test_device_frames_end_to_end(ns, nw):
     exe = os.path.join(BIN, "kv_cluster_device")

@@ -43,7 +43,8 @@ for st in "$@"; do
           python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" 10000000 gpurun_out/$out $per ;;
     f16) step 300 python3 bench.py --workload dense-f16 --no-cpu-baseline > gpurun_out/bench_f16.json 2> gpurun_out/bench_f16.err; echo "f16 rc=$?"; cat gpurun_out/bench_f16.json ;;
     e2e) step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 10000000 20 > gpurun_out/e2e_threads_10M.log 2>&1; echo "e2e threads rc=$?"; head -3 gpurun_out/e2e_threads_10M.log
-         step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 -procs 10000000 20 > gpurun_out/e2e_procs_10M.log 2>&1; echo "e2e procs rc=$?"; head -3 gpurun_out/e2e_procs_10M.log ;;
+         step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 -procs 10000000 20 > gpurun_out/e2e_procs_10M.log 2>&1; echo "e2e procs rc=$?"; head -3 gpurun_out/e2e_procs_10M.log
+         step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 10000000 20 1 > gpurun_out/e2e_threads_10M_keycache.log 2>&1; echo "e2e threads key-cache rc=$?"; head -3 gpurun_out/e2e_threads_10M_keycache.log ;;
     shared2|shared8)
           nr=${st#shared}; port=$((29500 + RANDOM % 1000))
           PSG_BENCH_SHARE_GPU=1 step 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $nr --master-addr 127.0.0.1 --master-port $port bench.py --gpus $nr > gpurun_out/bench_shared_n$nr.json 2> gpurun_out/bench_shared_n$nr.err; echo "$st rc=$?"; grep "^{" gpurun_out/bench_shared_n$nr.json | cut -c1-600 ;;
