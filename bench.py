@@ -112,15 +112,15 @@ class GpuBackend:
         self.vals = p.DeviceBuffer(L * self.vb)
         self.vals.fill_synth(L, self.dt, seed + self.rank, 0, 0.0, self.hi(), self.stream)
         self.out = p.DeviceBuffer(L * self.vb)
-        if self.cached:
-            if self.world > 1:
-                raise SystemExit("keyed-cached runs at N = 1 (one server)")
+        if self.cached and self.world == 1:
             # the first request of the key list: resolve it once, inserting the
             # keys (value 0, like the first Push's operator[]); later requests
             # run on the cached slots
             self.slots = p.DeviceBuffer(L * 4)
             self.store.resolve(self.keys, L, self.slots, insert=True, stream=self.stream)
-        if self.world > 1:
+        if self.world > 1 and self.cached:
+            self._setup_keyed_cached()
+        elif self.world > 1:
             if self.keyed and self.share_gpu:
                 raise SystemExit("the keyed N > 1 exchange runs on RCCL: one GPU per rank "
                                  "(PSG_BENCH_SHARE_GPU has no keyed path)")
@@ -184,6 +184,52 @@ class GpuBackend:
         self.xgmi, self.node_barrier = x, b
         self.node_barrier.wait()
 
+    def _setup_keyed_cached(self):
+        """configs[3] across GPUs with LR key caching: every worker pushes values
+        for the same key list; shard r resolves its segment (the DefaultSlicer's,
+        psg_slice) once to slots in its SORTED store, and the steady exchange is
+        the keyed xGMI pair psg_xgmi_push_slots / _pull_slots over the peers'
+        value vectors, stores and slot arrays (hipIpc)."""
+        import uuid
+        import numpy as np
+        p = self.p
+        kp = self._key_pos()
+        self.kp = [int(x) for x in kp]
+        lo, hi = self.kp[self.rank], self.kp[self.rank + 1]
+        self.seg = (lo, hi - lo)
+        if hi > lo:
+            tmp = p.DeviceBuffer((hi - lo) * self.vb)
+            # the list's first request inserts its keys (a Pull: operator[] with 0)
+            self.store.handle(p.PULL, self.keys.ptr + 8 * lo, None, tmp, hi - lo, stream=self.stream)
+            self.slots = p.DeviceBuffer((hi - lo) * 4)
+            self.store.resolve(self.keys.ptr + 8 * lo, hi - lo, self.slots, insert=False, stream=self.stream)
+        else:
+            self.slots = p.DeviceBuffer(4)
+        self.sync()
+        sptr = self.store.info().vals
+        mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr), p.ipc_export(self.slots.ptr))
+        allh = self.group.all_gather(mine)
+        tag = self.group.broadcast(uuid.uuid4().hex[:16] if self.rank == 0 else None)
+        self._peer_ptrs = []
+        vptrs, sptrs, self.peer_slots = [], [], []
+        for r in range(self.world):
+            if r == self.rank:
+                vptrs.append(self.vals.ptr)
+                sptrs.append(sptr)
+                self.peer_slots.append(self.slots.ptr)
+            else:
+                opened = [p.ipc_open(h) for h in allh[r]]
+                self._peer_ptrs += opened
+                vptrs.append(opened[0])
+                sptrs.append(opened[1])
+                self.peer_slots.append(opened[2])
+        self.xgmi = p.Xgmi(self.world, self.rank, vptrs, sptrs)
+        self.node_barrier = p.NodeBarrier("psg_bench_" + tag, self.world, self.rank)
+        self.seg_offs = np.array(self.kp[:-1], dtype=np.uint64)
+        self.seg_ns = np.array([self.kp[w + 1] - self.kp[w] for w in range(self.world)], dtype=np.uint64)
+        self.mode = "xgmi-keyed"
+        self.node_barrier.wait()
+
     def _key_pos(self):
         # the worker's DefaultSlicer on its HBM keys (psg_slice), every request
         kp, _ = self.p.slice_keys(self.keys, self.L, self.begins, self.ends, stream=self.stream)
@@ -191,6 +237,11 @@ class GpuBackend:
 
     # -- one phase at a time (N = 1, or the sequential RS / AG at N > 1)
     def push(self):
+        if self.mode == "xgmi-keyed":
+            self.xgmi.push_slots(self.store, self.slots, self.seg[0], self.seg[1], self.stream)
+            self.stream.sync()
+            self.node_barrier.wait()
+            return
         if self.mode == "xgmi":
             self.xgmi.push(self.store, self.L, self.stream)
             self.stream.sync()
@@ -212,6 +263,12 @@ class GpuBackend:
             self.comm.push(self.store, self.vals, self.L, self.scratch, self.stream)
 
     def pull(self):
+        if self.mode == "xgmi-keyed":
+            self.xgmi.pull_slots(self.store, self.peer_slots, self.seg_offs, self.seg_ns, self.out,
+                                 self.stream)
+            self.stream.sync()
+            self.node_barrier.wait()
+            return
         if self.mode == "xgmi":
             self.xgmi.pull(self.store, self.out, self.L, self.stream)
             self.stream.sync()
@@ -606,6 +663,9 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                                          "second HIP stream while chunk c+1's Push runs" % backend.nbuckets)
         elif getattr(backend, "mode", "rccl") == "xgmi":
             res["config"]["exchange"] = "one-shot xGMI kernels (psg_xgmi push/pull, peers via hipIpc)"
+        elif getattr(backend, "mode", "") == "xgmi-keyed":
+            res["config"]["exchange"] = ("keyed xGMI kernels on cached slots (psg_xgmi_push_slots / "
+                                         "_pull_slots over the peers' values, stores and slot lists)")
         elif getattr(backend, "keyed", False):
             res["config"]["exchange"] = "RCCL grouped reduce / broadcast of the key-range segments"
         else:

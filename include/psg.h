@@ -315,6 +315,20 @@ int psg_xgmi_push_range(psg_xgmi* x, psg_store* shard, uint64_t n_total, uint64_
                         uint64_t cnt, psg_stream stream);
 int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total,
                         uint64_t off, uint64_t cnt, psg_stream stream);
+/* Keyed exchange on cached slots (configs[3] with LR key caching): every rank
+ * pushes values for the SAME key list; [seg_off, seg_off + seg_n) is the
+ * psg_slice segment of this rank's shard, and `slots` its psg_store_resolve
+ * slots in this rank's SORTED store (registered as this rank's store array).
+ *   push: store[slots[i]] += vals_0[seg_off + i] + ... + vals_{N-1}[...]
+ *         (rank order: the N Push requests in arrival order 0..N-1)
+ *   pull: out[seg_off_w + i] = store_w[slots_w[i]] for every rank w
+ * peer_slots[w] is rank w's slot array mapped here (hipIpc).  The stores
+ * must not insert keys while mapped (an insert moves the value array). */
+int psg_xgmi_push_slots(psg_xgmi* x, psg_store* shard, const uint32_t* slots, uint64_t seg_off,
+                        uint64_t seg_n, psg_stream stream);
+int psg_xgmi_pull_slots(psg_xgmi* x, psg_store* shard, const uint32_t* const* peer_slots,
+                        const uint64_t* seg_off_host, const uint64_t* seg_n_host, void* out,
+                        psg_stream stream);
 /* Host barrier of the ranks of one node over a POSIX shared-memory page. */
 int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier** out);
 int psg_node_barrier_wait(psg_barrier* b, double timeout_s);

@@ -760,7 +760,9 @@ static int merge_insert(psg_store* s, const uint64_t* miss, uint64_t m, hipStrea
   uint64_t* K2 = nullptr;
   T* V2 = nullptr;
   PSG_HIP(hipMalloc((void**)&K2, (cap + kKeyPad) * sizeof(uint64_t)));
-  PSG_HIP(hipMalloc((void**)&V2, cap * sizeof(T)));
+  // whole 2 MiB pages: the value array is what peers map for the keyed xGMI
+  // exchange (psg_xgmi_push_slots / _pull_slots)
+  PSG_HIP(hipMalloc((void**)&V2, ipc_alloc_bytes(cap * sizeof(T))));
   if (S) k_merge_old<T><<<grid_n(S, kBlock), kBlock, 0, st>>>(s->keys, (const T*)s->vals, S, miss, m, K2, V2);
   k_merge_new<T><<<grid_n(m, kBlock), kBlock, 0, st>>>(s->keys, S, miss, m, K2, V2);
   PSG_HIP(hipGetLastError());

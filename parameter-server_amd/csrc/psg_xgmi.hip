@@ -85,6 +85,78 @@ __global__ __launch_bounds__(256) void k_xgmi_pull(u32x4* __restrict__ out, Peer
   }
 }
 
+// ---- keyed exchange on cached slots (LR key caching across GPUs) ------------
+// Every worker pushes values for the SAME key list (LR-like, configs[3]); the
+// list's segment r belongs to shard r, whose SORTED store resolved it once to
+// slots (psg_store_resolve).  Push: rank r reads segment r of every rank's
+// value vector in place and adds them in rank order to its store slots
+// (store[slot] + v_0 + v_1 + ..., the arrival order 0..N-1 of the N Push
+// requests, KVApp.h:446-449).  Pull: rank r gathers every owner's segment from
+// the owner's store through the owner's slots (KVApp.h:452 + the merge of
+// :713-720).  Four keys per lane; 16-B loads of the slots and values, and a
+// 16-B store read-modify-write when the four slots are consecutive.
+template <int DT>
+__global__ __launch_bounds__(256) void k_xgmi_push_slots(typename Elem<DT>::T* __restrict__ store,
+                                                         const uint32_t* __restrict__ slots, Peers src,
+                                                         int nsrc, uint64_t n, int vec) {
+  using E = Elem<DT>;
+  using T = typename E::T;
+  const uint64_t nq = vec ? n / 4 : 0;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  if constexpr (sizeof(T) == 4) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nq; j += stride) {
+      const u32x4 sl = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(slots) + j);
+      t4 v[kMaxPeers];
+#pragma unroll
+      for (int w = 0; w < kMaxPeers; ++w)
+        if (w < nsrc) v[w] = __builtin_bit_cast(t4, __builtin_nontemporal_load(src.p[w] + j));
+      const uint32_t p0 = sl[0];
+      if (sl[1] == p0 + 1 && sl[2] == p0 + 2 && sl[3] == p0 + 3 && (p0 & 3) == 0) {
+        u32x4* sp = reinterpret_cast<u32x4*>(store + p0);
+        t4 x = __builtin_bit_cast(t4, *sp);
+#pragma unroll
+        for (int w = 0; w < kMaxPeers; ++w)
+          if (w < nsrc) x = x + v[w];
+        *sp = __builtin_bit_cast(u32x4, x);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          T x = store[sl[k]];
+#pragma unroll
+          for (int w = 0; w < kMaxPeers; ++w)
+            if (w < nsrc) x = x + v[w][k];
+          store[sl[k]] = x;
+        }
+      }
+    }
+  }
+  for (uint64_t i = nq * 4 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const uint32_t p = slots[i];
+    T x = store[p];
+    for (int w = 0; w < nsrc; ++w) x = E::add1(x, reinterpret_cast<const T*>(src.p[w])[i]);
+    store[p] = x;
+  }
+}
+
+struct SlotPeers {
+  const uint32_t* slots[kMaxPeers];
+  uint64_t off[kMaxPeers];
+  uint64_t cnt[kMaxPeers];
+};
+
+// out[off_w + i] = store_w[slots_w[i]]; blockIdx.y = w.
+template <typename T>
+__global__ __launch_bounds__(256) void k_xgmi_pull_slots(T* __restrict__ out, Peers stores, SlotPeers sp) {
+  const int w = blockIdx.y;
+  const T* __restrict__ st = reinterpret_cast<const T*>(stores.p[w]);
+  const uint32_t* __restrict__ sl = sp.slots[w];
+  T* __restrict__ o = out + sp.off[w];
+  const uint64_t n = sp.cnt[w];
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+    o[i] = st[sl[i]];
+}
+
 }  // namespace psg
 
 struct psg_xgmi {
@@ -224,6 +296,73 @@ int psg_xgmi_lr_push(psg_xgmi* x, psg_store* weights, uint64_t n_total, float lr
   const float* g[kMaxPeers];
   for (int w = 0; w < x->nranks; ++w) g[w] = (const float*)x->vals[w] + (uint64_t)x->rank * blk;
   return lr_apply_sum(weights, 0, g, x->nranks, 1, blk, lr, adam, 0, iteration, (hipStream_t)stream);
+}
+
+int psg_xgmi_push_slots(psg_xgmi* x, psg_store* shard, const uint32_t* slots, uint64_t seg_off, uint64_t seg_n,
+                        psg_stream stream) {
+  PSG_REQUIRE(x && shard, PSG_ERR_INVALID, "psg_xgmi_push_slots: null argument");
+  PSG_REQUIRE(shard->vals == x->stores[x->rank], PSG_ERR_INVALID,
+              "psg_xgmi_push_slots: shard is not this rank's registered store");
+  if (seg_n == 0) return PSG_OK;
+  PSG_REQUIRE(slots, PSG_ERR_INVALID, "psg_xgmi_push_slots: null slots");
+  const int es = shard->esize;
+  Peers src;
+  bool vec = aligned16(slots) && aligned16(shard->vals) && es == 4;
+  for (int w = 0; w < x->nranks; ++w) {
+    src.p[w] = (const u32x4*)((const char*)x->vals[w] + seg_off * es);
+    vec = vec && aligned16(src.p[w]);
+  }
+  const uint64_t units = vec ? seg_n / 4 : seg_n;
+  uint64_t g = (units + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 4;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  hipStream_t st = (hipStream_t)stream;
+  switch (shard->dtype) {
+    case PSG_F32:
+      k_xgmi_push_slots<PSG_F32><<<(unsigned)g, kBlock, 0, st>>>((float*)shard->vals, slots, src, x->nranks, seg_n, vec);
+      break;
+    case PSG_F64:
+      k_xgmi_push_slots<PSG_F64><<<(unsigned)g, kBlock, 0, st>>>((double*)shard->vals, slots, src, x->nranks, seg_n, 0);
+      break;
+    case PSG_F16:
+      k_xgmi_push_slots<PSG_F16><<<(unsigned)g, kBlock, 0, st>>>((_Float16*)shard->vals, slots, src, x->nranks, seg_n, 0);
+      break;
+    default:
+      k_xgmi_push_slots<PSG_BF16><<<(unsigned)g, kBlock, 0, st>>>((__bf16*)shard->vals, slots, src, x->nranks, seg_n, 0);
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int psg_xgmi_pull_slots(psg_xgmi* x, psg_store* shard, const uint32_t* const* peer_slots,
+                        const uint64_t* seg_off_host, const uint64_t* seg_n_host, void* out, psg_stream stream) {
+  PSG_REQUIRE(x && shard && peer_slots && seg_off_host && seg_n_host && out, PSG_ERR_INVALID,
+              "psg_xgmi_pull_slots: null argument");
+  Peers st;
+  SlotPeers sp;
+  uint64_t most = 0;
+  for (int w = 0; w < x->nranks; ++w) {
+    PSG_REQUIRE(peer_slots[w] || seg_n_host[w] == 0, PSG_ERR_INVALID, "psg_xgmi_pull_slots: null slots of rank %d", w);
+    st.p[w] = (const u32x4*)x->stores[w];
+    sp.slots[w] = peer_slots[w];
+    sp.off[w] = seg_off_host[w];
+    sp.cnt[w] = seg_n_host[w];
+    most = seg_n_host[w] > most ? seg_n_host[w] : most;
+  }
+  if (most == 0) return PSG_OK;
+  uint64_t gx = (most + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 2 / (uint64_t)x->nranks + 1;
+  if (gx > cap) gx = cap;
+  const dim3 grid((unsigned)gx, (unsigned)x->nranks);
+  hipStream_t s = (hipStream_t)stream;
+  switch (shard->esize) {
+    case 4: k_xgmi_pull_slots<uint32_t><<<grid, kBlock, 0, s>>>((uint32_t*)out, st, sp); break;
+    case 8: k_xgmi_pull_slots<uint64_t><<<grid, kBlock, 0, s>>>((uint64_t*)out, st, sp); break;
+    default: k_xgmi_pull_slots<uint16_t><<<grid, kBlock, 0, s>>>((uint16_t*)out, st, sp); break;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
 }
 
 int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, uint64_t off,

@@ -50,7 +50,7 @@ EXPORTS = [
     "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
     "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_xgmi_push_range",
-    "psg_xgmi_pull_range", "psg_node_barrier_create",
+    "psg_xgmi_pull_range", "psg_xgmi_push_slots", "psg_xgmi_pull_slots", "psg_node_barrier_create",
     "psg_node_barrier_wait", "psg_node_barrier_destroy",
 ]
 
@@ -137,6 +137,8 @@ def lib() -> C.CDLL:
             "psg_xgmi_pull": ([vp, vp, vp, u64, vp], i32),
             "psg_xgmi_push_range": ([vp, vp, u64, u64, u64, vp], i32),
             "psg_xgmi_pull_range": ([vp, vp, vp, u64, u64, u64, vp], i32),
+            "psg_xgmi_push_slots": ([vp, vp, vp, u64, u64, vp], i32),
+            "psg_xgmi_pull_slots": ([vp, vp, C.POINTER(vp), vp, vp, vp, vp], i32),
             "psg_node_barrier_create": ([C.c_char_p, i32, i32, C.POINTER(vp)], i32),
             "psg_node_barrier_wait": ([vp, f64], i32), "psg_node_barrier_destroy": ([vp], i32),
         }
@@ -500,6 +502,17 @@ class Xgmi:
 
     def pull_range(self, shard: Store, out, n_total: int, off: int, cnt: int, stream=None) -> None:
         _call("psg_xgmi_pull_range", self.h, shard.h, _ptr(out), n_total, off, cnt, _s(stream))
+
+    def push_slots(self, shard: Store, slots, seg_off: int, seg_n: int, stream=None) -> None:
+        _call("psg_xgmi_push_slots", self.h, shard.h, _ptr(slots), seg_off, seg_n, _s(stream))
+
+    def pull_slots(self, shard: Store, peer_slots, seg_offs, seg_ns, out, stream=None) -> None:
+        w = len(peer_slots)
+        sl = (C.c_void_p * w)(*[_ptr(p) for p in peer_slots])
+        offs = np.ascontiguousarray(seg_offs, dtype=np.uint64)
+        ns = np.ascontiguousarray(seg_ns, dtype=np.uint64)
+        _call("psg_xgmi_pull_slots", self.h, shard.h, sl, offs.ctypes.data_as(C.c_void_p),
+              ns.ctypes.data_as(C.c_void_p), _ptr(out), _s(stream))
 
     def lr_push(self, weights: Store, n_total: int, lr: float, adam=None, iteration=0,
                 stream=None) -> None:
