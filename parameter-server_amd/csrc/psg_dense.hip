@@ -247,16 +247,19 @@ static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op) {
   if (store_bytes <= (512ull << 20)) {
     c.nt = 1;
   } else {
-    // past the Infinity Cache (profiles/r1_sweep_dense_256M.json and the
-    // Pull-only sweep profiles/r1_sweep_pull_256M.json): 1 vector per lane,
-    // all non-temporal; Push at 2 blocks/CU, Pull at 4 (0.80 of 8 TB/s, up
-    // from 0.72 with 2 vectors per lane)
+    // past the Infinity Cache, all non-temporal.  Pull (the Pull-only sweep
+    // profiles/r1_sweep_pull_256M.json): 1 vector per lane at 4 blocks/CU
+    // (0.80 of 8 TB/s, up from 0.72 with 2 vectors per lane).  Push: 2 vectors
+    // per lane at 2 blocks/CU — consecutive Pushes into one store (several
+    // workers in a row) run at 0.770 of HBM against 0.686 with 1 vector
+    // (profiles/r2_sweep_b2b_push_256M.json), for 0.774 vs 0.786 when a Pull
+    // sits between them (profiles/r1_sweep_dense_256M.json)
     c.nt = 3;
     if (op == PSG_PULL) {
       c.unroll = 1;
       c.blocks_per_cu = 4;
     } else {
-      c.unroll = 1;
+      c.unroll = 2;
       c.blocks_per_cu = 2;
     }
   }
