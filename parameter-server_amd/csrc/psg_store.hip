@@ -23,7 +23,9 @@
 //           applied to exactly those keys.
 //   Rejected requests (unsorted, duplicate, out-of-range keys) leave the store
 //   unchanged: the validation pass raises a device word that every
-//   store-writing kernel of the request checks first.
+//   store-writing kernel of the request checks first.  A Pull, which writes
+//   only its reply, skips that pass: k_resolve_apply checks its keys on the
+//   way (the reply of a rejected Pull is unspecified, as no reply is sent).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -314,10 +316,16 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
   constexpr uint32_t winN = 2 * NT * kPerLane;          // LDS window of store keys
   __shared__ uint64_t sK[winN];
-  // k_validate_windows rejected the request: write nothing (a uniform early
-  // exit of every block before any store access)
-  if (*reject == seq) return;
-  int missing = 0;
+  // A request that writes the store was validated as a whole first: if
+  // k_validate_windows rejected it, write nothing (a uniform early exit of
+  // every block before any store access).  A Pull writes only its reply, so
+  // it checks its keys here, in the same pass (CHECK), and the host rejects it
+  // from the flags before anything else happens (no insert of absent keys).
+  constexpr bool CHECK = OP == PSG_PULL;
+  if constexpr (!CHECK) {
+    if (*reject == seq) return;
+  }
+  int missing = 0, range = 0, unsorted = 0;
   const uint64_t ntiles = (n + tileN - 1) / tileN;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * tileN;
@@ -360,6 +368,27 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
     } else {
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : 0;
+    }
+    if constexpr (CHECK) {
+      // strict ascent against the key before this lane's four (the previous
+      // lane's last, by a shuffle; lane 0 of a wave loads it) and the range
+      const uint64_t last = key[kPerLane - 1];
+      const uint32_t plo = __shfl_up((uint32_t)last, 1, 64), phi = __shfl_up((uint32_t)(last >> 32), 1, 64);
+      uint64_t prev = ((uint64_t)phi << 32) | plo;
+      bool have_prev = true;
+      if ((threadIdx.x & 63) == 0) {
+        have_prev = i0 > 0 && i0 < t1;
+        prev = have_prev ? q[i0 - 1] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        if (i0 + k < t1) {
+          if (key[k] < kb || key[k] >= ke) range = 1;
+          if (have_prev && prev >= key[k]) unsorted = 1;
+          prev = key[k];
+          have_prev = true;
+        }
+      }
     }
     T v[kPerLane];
     if constexpr ((OP & PSG_PUSH) != 0) {
@@ -466,6 +495,10 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
     __syncthreads();
   }
   raise_flag(flags, F_MISSING, missing != 0);
+  if constexpr (CHECK) {
+    raise_flag(flags, F_RANGE, range != 0);
+    raise_flag(flags, F_UNSORTED, unsorted != 0);
+  }
 }
 
 // Block-wide exclusive scan helper over 256 lanes (wave = 64).
@@ -867,7 +900,8 @@ static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, co
   // search blocks: one wave per window bound (ntiles + 1 of them); key-stream
   // blocks: 1024 keys each, capped at the streaming grid
   const unsigned nsearch = (unsigned)((ntiles + 1 + kBlock / 64 - 1) / (kBlock / 64));
-  const unsigned nval = grid_n(n, (uint64_t)kBlock * 8);
+  // a Pull checks its keys inside k_resolve_apply: window searches only
+  const unsigned nval = op == PSG_PULL ? 0u : grid_n(n, (uint64_t)kBlock * 8);
   k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, tile, nsearch,
                                                        s->key_begin, s->key_end, s->reject_dev, seq, s->flags,
                                                        aligned16(q) ? 1 : 0);

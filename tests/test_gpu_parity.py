@@ -232,15 +232,17 @@ def test_sorted_rejects_duplicate_keys():
     assert ei.value.code == 1 and "ascending" in str(ei.value)
 
 
-@pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL])
+@pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL])
 @pytest.mark.parametrize("bad", ["duplicate_last_tile", "unsorted_middle", "out_of_range_last",
-                                 "duplicate_adjacent_lanes"])
+                                 "duplicate_adjacent_lanes", "duplicate_adjacent_waves"])
 def test_sorted_rejected_request_leaves_a_populated_store_unchanged(bad, flags):
     """The KVPairs contract (KVApp.h:23): keys strictly ascending.  A request that
     breaks it — or names a key outside the shard — is rejected as a whole
     (k_validate_windows runs over every key before k_resolve_apply writes), so
     the store keeps exactly what it held, even when the bad key sits in the
-    last of many request tiles."""
+    last of many request tiles.  A Pull checks its keys inside k_resolve_apply
+    (lane to lane by a shuffle, wave to wave by a load) and is rejected before
+    any absent key is inserted."""
     rng = np.random.default_rng(41)
     kb, ke = 1000, 1 << 62
     univ = np.unique(rng.integers(kb, ke, 60000, dtype=np.uint64))
@@ -254,8 +256,10 @@ def test_sorted_rejected_request_leaves_a_populated_store_unchanged(bad, flags):
         k[30000], k[30001] = k[30001], k[30000]
     elif bad == "out_of_range_last":
         k[-1] = ke + 5
-    else:
+    elif bad == "duplicate_adjacent_lanes":
         k[4100] = k[4099]  # the last key of lane 0 and the first of lane 1, second tile
+    else:
+        k[4096 + 256] = k[4096 + 255]  # the last key of wave 0 and the first of wave 1
     n = len(k)
     out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
     with pytest.raises(psg.PsgError) as ei:
