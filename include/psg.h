@@ -172,6 +172,8 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * (dense request: no key array travels).  Keys must be strictly ascending
  * (KVPairs contract, KVApp.h:23); a PULL of an absent key inserts it with 0.
  * A DENSE store accepts only keys inside [key_begin, key_begin + capacity).
+ * A request that breaks either rule fails (PSG_ERR_INVALID / PSG_ERR_RANGE)
+ * and leaves the store unchanged; the contents of out are then unspecified.
  * vals/out are device arrays of n elements of the store's dtype. */
 int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,
                      uint64_t first_key, const void* vals, void* out, uint64_t n,

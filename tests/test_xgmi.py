@@ -46,7 +46,7 @@ def test_node_barrier_cpu():
     assert sorted(out.get(timeout=5) for _ in range(3)) == [0, 1, 2]
 
 
-def _xgmi_rank(rank, world, n, steps, name, q_in, q_out):
+def _xgmi_rank(rank, world, n, steps, name, q_in, q_out, mode=0):
     _paths()
     import oracle
     import psg
@@ -55,7 +55,8 @@ def _xgmi_rank(rank, world, n, steps, name, q_in, q_out):
     psg.set_device(rank % psg.device_count())
     blk = n // world
     vals = psg.DeviceBuffer(n * 4)
-    vals.fill_synth(n, psg.F32, 7 + rank, 0, 0.0, 1000.0)
+    lo_v, hi_v = (0.0, 1000.0) if mode == 0 else (-1.0, 1.0)
+    vals.fill_synth(n, psg.F32, 7 + rank, mode, lo_v, hi_v)
     store = psg.Store(psg.DENSE, psg.F32, rank * blk, (rank + 1) * blk, blk)
     sptr = store.info().vals
     psg.device_sync()
@@ -76,7 +77,7 @@ def _xgmi_rank(rank, world, n, steps, name, q_in, q_out):
         bar.wait()
     got = out.download(np.float32, n)
     exp = np.zeros(n, np.float32)
-    ref = [oracle.synth(n, oracle.F32, 7 + w, 0, 0.0, 1000.0) for w in range(world)]
+    ref = [oracle.synth(n, oracle.F32, 7 + w, mode, lo_v, hi_v) for w in range(world)]
     for r in range(world):  # shard r: `steps` pushes of every worker, in rank order
         st = oracle.Store(oracle.F32)
         lo = r * blk
@@ -96,14 +97,19 @@ def _xgmi_rank(rank, world, n, steps, name, q_in, q_out):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_xgmi_exchange_multiprocess(world):
+@pytest.mark.parametrize("world,mode", [(2, 0), (3, 0), (2, 1), (3, 1)])
+def test_xgmi_exchange_multiprocess(world, mode):
+    """Every rank's Push lands on every shard and every Pull reads every shard.
+    mode 0: integer-valued data (the reference KATs); mode 1: real-valued
+    U(-1, 1).  k_xgmi_push adds the sources to the shard one at a time in rank
+    order, which is the oracle's order of sequential pushes, so both are
+    bit-exact (no 1e-6 tolerance needed)."""
     n = 3 * 64 * 4096  # divisible by 2 and 3, 16-B blocks
     ctx = mp.get_context("spawn")
     q_out = ctx.Queue()
     q_in = [ctx.Queue() for _ in range(world)]
     name = "psg_xgmi_" + uuid.uuid4().hex[:12]
-    procs = [ctx.Process(target=_xgmi_rank, args=(r, world, n, 3, name, q_in[r], q_out))
+    procs = [ctx.Process(target=_xgmi_rank, args=(r, world, n, 3, name, q_in[r], q_out, mode))
              for r in range(world)]
     for p in procs:
         p.start()
