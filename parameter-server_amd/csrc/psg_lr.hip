@@ -19,6 +19,7 @@
 // Bytes per feature: merged f32 4 + weight f32 r/w 8 (+ m, v f64 r/w 32 with
 // Adam): HBM-bound, streamed.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "psg_internal.h"
@@ -31,53 +32,100 @@ namespace psg {
 //       the arrival order of merge_buf_.vals[i] += req_data.vals[i], LRServer.h:158-160;
 //       ZERO = the sync merge buffer that starts at 0, else async's raw push)
 //   grad = (double)(lr * s); Adam (LRServer.h:171-174); w = (float)((double)w - grad)
-// Four features per lane as 16-B vectors (f32 w / g, two f64x2 each for Adam's
-// m and v); every gradient's loads are issued before the adds.  Bytes per
+// SGD: four features per lane as 16-B vectors; Adam: two pairs per lane (see
+// below); every gradient's loads are issued before the adds.  Bytes per
 // feature: 4 * ng + 8 (+ 32 with Adam) — HBM-bound.
-template <bool ADAM, bool ZERO>
+// the model's own arrays (w, m, v): non-temporal once they are well past the
+// Infinity Cache (nt), default policy while a round's state can stay in it
+template <typename V>
+__device__ __forceinline__ V ld_nt(const V* p, int nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename V>
+__device__ __forceinline__ void st_nt(V* p, V x, int nt) {
+  if (nt) __builtin_nontemporal_store(x, p);
+  else *p = x;
+}
+
+// MAXG: gradient slots the kernel keeps registers for (4 when ng <= 4: 125 ->
+// fewer VGPRs, more waves in flight; else kMaxGrads).
+template <bool ADAM, bool ZERO, int MAXG>
 __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Grads g, int ng, uint64_t n,
                                                       float lr, double* __restrict__ m,
                                                       double* __restrict__ v, double alr, double b1,
                                                       double b2, double eps, double c1, double c2,
-                                                      int vec) {
+                                                      int vec, int nt) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const uint64_t nv = vec ? n / 4 : 0;
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nv; j += stride) {
-    f32x4 x[kMaxGrads];
+  uint64_t done = 0;  // features the vector loop covers
+  if constexpr (!ADAM) {
+    const uint64_t nv = vec ? n / 4 : 0;
+    done = nv * 4;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nv; j += stride) {
+      f32x4 x[MAXG];
 #pragma unroll
-    for (int k = 0; k < kMaxGrads; ++k)
-      if (k < ng)
-        x[k] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(g.p[k]) + j));
-    f32x4 s = ZERO ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} + x[0] : x[0];
+      for (int k = 0; k < MAXG; ++k)
+        if (k < ng)
+          x[k] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(g.p[k]) + j));
+      f32x4 s = ZERO ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} + x[0] : x[0];
 #pragma unroll
-    for (int k = 1; k < kMaxGrads; ++k)
-      if (k < ng) s = s + x[k];
-    f32x4 wv = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(w + 4 * j));
-    double gr[4];
+      for (int k = 1; k < MAXG; ++k)
+        if (k < ng) s = s + x[k];
+      f32x4 wv = __builtin_bit_cast(f32x4, ld_nt(reinterpret_cast<const u32x4*>(w + 4 * j), nt));
 #pragma unroll
-    for (int e = 0; e < 4; ++e) gr[e] = (double)(lr * s[e]);
-    if constexpr (ADAM) {
-      f64x2* mp = reinterpret_cast<f64x2*>(m + 4 * j);
-      f64x2* vp = reinterpret_cast<f64x2*>(v + 4 * j);
-      f64x2 mm[2] = {mp[0], mp[1]}, vv[2] = {vp[0], vp[1]};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const double mi = b1 * mm[e >> 1][e & 1] + (1.0 - b1) * gr[e];
-        const double vi = b2 * vv[e >> 1][e & 1] + (1.0 - b2) * gr[e] * gr[e];
-        mm[e >> 1][e & 1] = mi;
-        vv[e >> 1][e & 1] = vi;
-        gr[e] = alr * (mi / c1) / (sqrt(vi / c2) + eps);
-      }
-      mp[0] = mm[0];
-      mp[1] = mm[1];
-      vp[0] = vv[0];
-      vp[1] = vv[1];
+      for (int e = 0; e < 4; ++e) wv[e] = (float)((double)wv[e] - (double)(lr * s[e]));
+      st_nt(reinterpret_cast<u32x4*>(w + 4 * j), __builtin_bit_cast(u32x4, wv), nt);
     }
+  } else {
+    // Adam: 256 features per wave, lane l owning features 2l, 2l+1 of each
+    // 128-feature half, so every load and store instruction of a wave is one
+    // contiguous run (512 B of f32 pairs, 1 KiB of f64 pairs).  With four
+    // consecutive features per lane the f64 moments moved at a 32-B lane
+    // stride, each instruction writing half of every line (0.63 of HBM at 64 M
+    // features).
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const uint64_t nu = vec ? n / 256 * 64 : 0;  // lane units of whole wave tiles
+    done = nu * 4;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nu; j += stride) {
+      const uint64_t f0 = (j >> 6) * 256 + 2 * (j & 63);  // first pair; the second is f0 + 128
+      f32x2 x[MAXG][2];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) wv[e] = (float)((double)wv[e] - gr[e]);
-    *reinterpret_cast<u32x4*>(w + 4 * j) = __builtin_bit_cast(u32x4, wv);
+      for (int k = 0; k < MAXG; ++k)
+        if (k < ng)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            x[k][h] = __builtin_bit_cast(
+                f32x2, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g.p[k] + f0 + 128 * h)));
+      f32x2 wv[2];
+      f64x2 mm[2], vv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        wv[h] = __builtin_bit_cast(f32x2, ld_nt(reinterpret_cast<const u32x2*>(w + f0 + 128 * h), nt));
+        mm[h] = ld_nt(reinterpret_cast<const f64x2*>(m + f0 + 128 * h), nt);
+        vv[h] = ld_nt(reinterpret_cast<const f64x2*>(v + f0 + 128 * h), nt);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x2 s = ZERO ? f32x2{0.0f, 0.0f} + x[0][h] : x[0][h];
+#pragma unroll
+        for (int k = 1; k < MAXG; ++k)
+          if (k < ng) s = s + x[k][h];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double gr = (double)(lr * s[e]);
+          const double mi = b1 * mm[h][e] + (1.0 - b1) * gr;
+          const double vi = b2 * vv[h][e] + (1.0 - b2) * gr * gr;
+          mm[h][e] = mi;
+          vv[h][e] = vi;
+          wv[h][e] = (float)((double)wv[h][e] - alr * (mi / c1) / (sqrt(vi / c2) + eps));
+        }
+        st_nt(reinterpret_cast<f64x2*>(m + f0 + 128 * h), mm[h], nt);
+        st_nt(reinterpret_cast<f64x2*>(v + f0 + 128 * h), vv[h], nt);
+        st_nt(reinterpret_cast<u32x2*>(w + f0 + 128 * h), __builtin_bit_cast(u32x2, wv[h]), nt);
+      }
+    }
   }
-  for (uint64_t i = nv * 4 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+  for (uint64_t i = done + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     float s = ZERO ? 0.0f + g.p[0][i] : g.p[0][i];
     for (int k = 1; k < ng; ++k) s = s + g.p[k][i];
     double grad = (double)(lr * s);
@@ -130,19 +178,33 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   const uint64_t cap = (uint64_t)max_stream_blocks();
   const unsigned grid = (unsigned)(b < cap ? (b ? b : 1) : cap);
   const int ve = vec ? 1 : 0;
+  // PSG_LR_NT=0/1 forces the policy (sweeps); default: non-temporal when the
+  // model's arrays exceed 512 MiB
+  static const int nt_env = [] {
+    const char* e = getenv("PSG_LR_NT");
+    return e ? atoi(e) : -1;
+  }();
+  const uint64_t state_bytes = n * (adam ? 20ull : 4ull);
+  const int ntm = nt_env >= 0 ? (nt_env ? 1 : 0) : (state_bytes > (512ull << 20) ? 1 : 0);
   const double alr = adam ? adam->lr : 0, b1 = adam ? adam->beta1 : 0, b2 = adam ? adam->beta2 : 0,
                eps = adam ? adam->eps : 0;
-  if (adam) {
-    if (from_zero)
-      k_lr_apply_sum<true, true><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve);
-    else
-      k_lr_apply_sum<true, false><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve);
+#define PSG_LR_LAUNCH(A, Z, G)                                                                        \
+  k_lr_apply_sum<A, Z, G><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
+  const bool few = ngrads <= 4;
+  if (adam && from_zero) {
+    if (few) PSG_LR_LAUNCH(true, true, 4);
+    else PSG_LR_LAUNCH(true, true, kMaxGrads);
+  } else if (adam) {
+    if (few) PSG_LR_LAUNCH(true, false, 4);
+    else PSG_LR_LAUNCH(true, false, kMaxGrads);
+  } else if (from_zero) {
+    if (few) PSG_LR_LAUNCH(false, true, 4);
+    else PSG_LR_LAUNCH(false, true, kMaxGrads);
   } else {
-    if (from_zero)
-      k_lr_apply_sum<false, true><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, 0, 0, 0, 0, 1, 1, ve);
-    else
-      k_lr_apply_sum<false, false><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, 0, 0, 0, 0, 1, 1, ve);
+    if (few) PSG_LR_LAUNCH(false, false, 4);
+    else PSG_LR_LAUNCH(false, false, kMaxGrads);
   }
+#undef PSG_LR_LAUNCH
   PSG_HIP(hipGetLastError());
   return PSG_OK;
 }
