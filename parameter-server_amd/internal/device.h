@@ -28,6 +28,14 @@ void EnableAllPeerAccess();
 /* kind: 0 H2D, 1 D2H, 2 D2D, 3 default; synchronises the thread stream */
 void CopySync(void* dst, const void* src, size_t bytes, int kind = 3);
 
+/* Pipelined copies between a pageable host array and HBM: chunks go through
+ * two pinned staging blocks of the calling thread, so the host copy of chunk
+ * c + 1 (HostCopy, several threads) runs while chunk c is on PCIe.  Return
+ * when the data has landed.  Used for the host-vector forms of KVWorker's
+ * Push / Pull / PushPull on a node with a GPU. */
+void StageToDevice(void* dst_dev, const void* src_host, size_t bytes);
+void StageToHost(void* dst_host, const void* src_dev, size_t bytes);
+
 /* DefaultSlicer positions for a device key array (psg_slice) */
 void SliceKeys(const uint64_t* keys, size_t n, const int* lens, size_t num_vals,
                const std::vector<Range>& ranges, std::vector<uint64_t>* key_pos,

@@ -18,6 +18,7 @@
 // that can consume HBM frames registers with SetDeviceRequestHandle.
 #pragma once
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -88,6 +89,24 @@ SVector<T> ToDeviceAsync(const SVector<T>& v, int dev) {
                 "psg_memcpy H2D");
   return d;
 }
+// The copy a host-vector Push / Pull makes of the caller's array
+// (KVApp.h:119-121, 155).  On a node with a GPU, a large array (>= 4 MiB) is
+// copied straight into HBM by the pipelined staging (device::StageToDevice):
+// the request then takes the HBM path (device slicer, HBM frames, no H2D on
+// the server) and the host copy overlaps the PCIe transfer.  Elsewhere, or
+// with PS_STAGE_TO_HBM=0, it is the reference's host SVector copy.
+template <typename T>
+SVector<T> StageFrame(const std::vector<T>& v) {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_STAGE_TO_HBM");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const int dev = PostOffice::Get()->device();
+  if (!on || dev < 0 || v.size() * sizeof(T) < (size_t(4) << 20)) return SVector<T>(v);
+  SVector<T> d = SVector<T>::OnDevice(v.size(), dev);
+  device::StageToDevice(d.data(), v.data(), v.size() * sizeof(T));
+  return d;
+}
 // The key-list hash of LR key caching: the std::hash<ps::SVector<uint64_t>>
 // specialisation of tests/src/LRServer.h:11-29, which the reference worker
 // also uses (LRWorker.h:214-219), restated so a server finds the list a
@@ -126,17 +145,19 @@ class KVWorker : public SimpleApp {
     customer_ = nullptr;
   }
 
-  /* KVApp.h:112-122: the vectors are copied into SVectors */
+  /* KVApp.h:112-122: the vectors are copied into SVectors (into HBM on a
+   * node with a GPU, detail::StageFrame; the lens stay on the host) */
   int Push(const std::vector<Key>& keys, const std::vector<Value>& vals,
            const std::vector<int>& lens = {}, int cmd = 0, const Callback& cb = nullptr,
            int priority = 0) {
-    return ZPush(SVector<Key>(keys), SVector<Value>(vals), SVector<int>(lens), cmd, cb, priority);
+    if (!lens.empty()) return ZPush(SVector<Key>(keys), SVector<Value>(vals), SVector<int>(lens), cmd, cb, priority);
+    return ZPush(detail::StageFrame(keys), detail::StageFrame(vals), SVector<int>(), cmd, cb, priority);
   }
 
   /* KVApp.h:148-162 */
   int Pull(const std::vector<Key>& keys, std::vector<Value>* vals, std::vector<int>* lens = nullptr,
            int cmd = 0, const Callback& cb = nullptr, int priority = 0) {
-    SVector<Key> skeys(keys);
+    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys);
     int ts = AddPullCB(skeys, vals, lens, cmd, cb);
     Data kvs;
     kvs.keys = skeys;
@@ -154,8 +175,8 @@ class KVWorker : public SimpleApp {
       outs->resize(vals.size());
     else
       CHECK_EQ(vals.size(), outs->size());
-    SVector<Key> skeys(keys);
-    SVector<Value> svals(vals);
+    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys);
+    SVector<Value> svals = lens ? SVector<Value>(vals) : detail::StageFrame(vals);
     auto souts = new SVector<Value>(outs->data(), outs->size());
     SVector<int>* slens = lens ? new SVector<int>(lens->data(), lens->size()) : nullptr;
     return ZPushPull(skeys, svals, souts, slens, cmd,
@@ -687,7 +708,7 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
     } else {
       SVector<Value> tmp = SVector<Value>::OnDevice(total_val, my_dev);
       device::Merge(&segs, sizeof(Value), tmp.data(), total_val);
-      device::CopySync(vals->data(), tmp.data(), total_val * sizeof(Value), 1);
+      device::StageToHost(vals->data(), tmp.data(), total_val * sizeof(Value));
     }
   }
   if (lens) {

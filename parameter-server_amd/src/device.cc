@@ -52,7 +52,6 @@ thread_local ThreadStreams t_streams;
 struct Pool {
   std::mutex mu;
   std::map<std::pair<int, size_t>, std::vector<void*>> free;
-  std::map<size_t, uint64_t> seen;  // pinned-host requests per size class
   std::map<size_t, bool> pinning;   // a block of this class is being pinned
   static size_t Round(size_t b) {
     if (b <= (64u << 20)) return (b + 65535) & ~size_t(65535);
@@ -132,11 +131,11 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
       p = fl.back();
       fl.pop_back();
     } else {
-      // pinning costs far more than one copy and must not stall a request: a
-      // size class seen before gets a block pinned in the background, which
-      // the next request of that size picks up (a training loop); this one
-      // stays pageable (a one-shot Push, test_kv_app_benchmark's repeat = 1)
-      if (pool.seen[rb]++ > 0 && !pool.pinning[rb]) {
+      // pinning costs far more than one copy and must not stall a request:
+      // the size class gets a block pinned in the background, which a later
+      // request of that size picks up (a training loop); this one stays
+      // pageable (a one-shot Push, test_kv_app_benchmark's repeat = 1)
+      if (!pool.pinning[rb]) {
         pool.pinning[rb] = true;
         std::thread([rb] {
           void* q = nullptr;
@@ -179,6 +178,77 @@ void CopySync(void* dst, const void* src, size_t bytes, int kind) {
   psg_stream s = ThreadStream();
   Check(psg_memcpy(dst, src, bytes, kind, s), "psg_memcpy");
   Check(psg_stream_sync(s), "psg_stream_sync");
+}
+
+namespace {
+// Two pinned staging blocks per thread and the events that tell when the DMA
+// out of / into each one is done.  Kept for the thread's life (like its stream).
+constexpr size_t kStageChunk = size_t(16) << 20;
+struct Staging {
+  void* block[2] = {nullptr, nullptr};
+  psg_event done[2] = {nullptr, nullptr};
+  bool pending[2] = {false, false};
+  bool ok = false;
+  bool tried = false;
+};
+thread_local Staging t_stage;
+
+Staging* GetStaging() {
+  Staging& st = t_stage;
+  if (!st.tried) {
+    st.tried = true;
+    st.ok = true;
+    for (int b = 0; b < 2 && st.ok; ++b)
+      st.ok = psg_host_alloc(&st.block[b], kStageChunk) == PSG_OK && psg_event_create(&st.done[b]) == PSG_OK;
+  }
+  return st.ok ? &st : nullptr;
+}
+}  // namespace
+
+void StageToDevice(void* dst_dev, const void* src_host, size_t bytes) {
+  if (!bytes) return;
+  psg_stream s = ThreadStream();
+  Staging* st = GetStaging();
+  if (!st) {  // no pinned memory: the runtime's own pageable path
+    CopySync(dst_dev, src_host, bytes, 0);
+    return;
+  }
+  int b = 0;
+  for (size_t off = 0; off < bytes; off += kStageChunk, b ^= 1) {
+    const size_t len = std::min(kStageChunk, bytes - off);
+    if (st->pending[b]) Check(psg_event_sync(st->done[b]), "psg_event_sync");  // block b's last DMA
+    HostCopy(st->block[b], (const char*)src_host + off, len);
+    Check(psg_memcpy((char*)dst_dev + off, st->block[b], len, 0, s), "psg_memcpy H2D");
+    Check(psg_event_record(st->done[b], s), "psg_event_record");
+    st->pending[b] = true;
+  }
+  Check(psg_stream_sync(s), "psg_stream_sync");
+  st->pending[0] = st->pending[1] = false;
+}
+
+void StageToHost(void* dst_host, const void* src_dev, size_t bytes) {
+  if (!bytes) return;
+  psg_stream s = ThreadStream();
+  Staging* st = GetStaging();
+  if (!st) {
+    CopySync(dst_host, src_dev, bytes, 1);
+    return;
+  }
+  const size_t n = (bytes + kStageChunk - 1) / kStageChunk;
+  auto issue = [&](size_t c) {
+    const size_t off = c * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    Check(psg_memcpy(st->block[c & 1], (const char*)src_dev + off, len, 1, s), "psg_memcpy D2H");
+    Check(psg_event_record(st->done[c & 1], s), "psg_event_record");
+  };
+  issue(0);
+  for (size_t c = 0; c < n; ++c) {
+    // chunk c + 1 goes on PCIe while chunk c is copied out of its block
+    if (c + 1 < n) issue(c + 1);
+    Check(psg_event_sync(st->done[c & 1]), "psg_event_sync");
+    const size_t off = c * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    HostCopy((char*)dst_host + off, st->block[c & 1], len);
+  }
+  st->pending[0] = st->pending[1] = false;
 }
 
 void SliceKeys(const uint64_t* keys, size_t n, const int* lens, size_t num_vals,

@@ -87,17 +87,23 @@ int main(int argc, char* argv[]) {
     kv.Wait(kv.Push(hkeys, hvals));
     kv.Wait(kv.Pull(hkeys, &rets));
     if (key_cache) hkeys = std::vector<Key>{detail::KeyListHash(hkeys.data(), hkeys.size())};
+    // warm-up in the timed form (the hashed list names reply frames of a size
+    // the pinned host pool has not seen yet)
+    for (int w = 0; w < 3; ++w) {
+      kv.Wait(kv.Push(hkeys, hvals));
+      kv.Wait(kv.Pull(hkeys, &rets));
+    }
     t0 = clk::now();
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.Push(hkeys, hvals));
     double hpush = ms_since(t0) / repeat;
     t0 = clk::now();
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.Pull(hkeys, &rets));
     double hpull = ms_since(t0) / repeat;
-    for (long i = 0; i < num; ++i) CHECK_EQ(rets[i], hvals[i] * (repeat + 1)) << "host path, i=" << i;
+    for (long i = 0; i < num; ++i) CHECK_EQ(rets[i], hvals[i] * (repeat + 4)) << "host path, i=" << i;
     std::vector<float> outs;
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.PushPull(hkeys, hvals, &outs));
     for (long i = 0; i < num; ++i)
-      CHECK_EQ(outs[i], hvals[i] * (2 * repeat + 1)) << "host push-pull, i=" << i;
+      CHECK_EQ(outs[i], hvals[i] * (2 * repeat + 4)) << "host push-pull, i=" << i;
 
     std::printf("{\"rank\": %d, \"n\": %ld, \"servers\": %d, \"key_cache\": %d, \"device_push_ms\": %.4f, "
                 "\"device_pull_ms\": %.4f, \"host_push_ms\": %.4f, \"host_pull_ms\": %.4f}\n",
