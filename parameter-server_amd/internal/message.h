@@ -73,6 +73,7 @@ struct Meta {
   bool push = false;
   bool pull = false;
   bool simple_app = false;
+  bool hbm_handle = false;     // a reply from a server whose handle takes HBM frames
   std::string body;
   std::vector<DataType> data_type;
   Control control;

@@ -8,9 +8,10 @@
 //           arrays in HBM; one message per non-empty slice (frames zero-copy).
 //   server  KVServerDefaultHandle keeps the value store in HBM (psg_store,
 //           SORTED layout) and runs every request as the psg_store_handle
-//           kernel.  Host frames are staged into HBM first; HBM frames (a
-//           worker that holds its keys / values on a GPU) are read in place,
-//           over xGMI when the worker's GPU is another one.
+//           kernel.  HBM frames (a worker that holds its keys / values on a
+//           GPU, or a host-vector request the worker staged into HBM,
+//           detail::StageFrame) are read in place, over xGMI when the
+//           worker's GPU is another one; host frames are copied into HBM.
 //   merge   Pull replies are concatenated in key order: memcpy for host
 //           replies (KVApp.h:713-720), the psg_merge kernel for HBM replies.
 // Custom request handles registered with SetRequestHandle see host frames
@@ -18,6 +19,7 @@
 // that can consume HBM frames registers with SetDeviceRequestHandle.
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -90,19 +92,22 @@ SVector<T> ToDeviceAsync(const SVector<T>& v, int dev) {
   return d;
 }
 // The copy a host-vector Push / Pull makes of the caller's array
-// (KVApp.h:119-121, 155).  On a node with a GPU, a large array (>= 4 MiB) is
-// copied straight into HBM by the pipelined staging (device::StageToDevice):
-// the request then takes the HBM path (device slicer, HBM frames, no H2D on
-// the server) and the host copy overlaps the PCIe transfer.  Elsewhere, or
-// with PS_STAGE_TO_HBM=0, it is the reference's host SVector copy.
+// (KVApp.h:119-121, 155).  On a node with a GPU, once every server has
+// answered that its handle takes HBM frames (Meta::hbm_handle: the default
+// handle, SetDeviceRequestHandle), a large array (>= 4 MiB) is copied straight
+// into HBM by the pipelined staging (device::StageToDevice): the request then
+// takes the HBM path (device slicer, HBM frames, no H2D on the server) and the
+// host copy overlaps the PCIe transfer.  Otherwise — a host handle such as
+// test_kv_app_benchmark's, which would copy the frames back — or with
+// PS_STAGE_TO_HBM=0, it is the reference's host SVector copy.
 template <typename T>
-SVector<T> StageFrame(const std::vector<T>& v) {
+SVector<T> StageFrame(const std::vector<T>& v, bool servers_take_hbm) {
   static const bool on = [] {
     const char* e = std::getenv("PS_STAGE_TO_HBM");
     return !(e && std::atoi(e) == 0);
   }();
   const int dev = PostOffice::Get()->device();
-  if (!on || dev < 0 || v.size() * sizeof(T) < (size_t(4) << 20)) return SVector<T>(v);
+  if (!on || !servers_take_hbm || dev < 0 || v.size() * sizeof(T) < (size_t(4) << 20)) return SVector<T>(v);
   SVector<T> d = SVector<T>::OnDevice(v.size(), dev);
   device::StageToDevice(d.data(), v.data(), v.size() * sizeof(T));
   return d;
@@ -151,13 +156,14 @@ class KVWorker : public SimpleApp {
            const std::vector<int>& lens = {}, int cmd = 0, const Callback& cb = nullptr,
            int priority = 0) {
     if (!lens.empty()) return ZPush(SVector<Key>(keys), SVector<Value>(vals), SVector<int>(lens), cmd, cb, priority);
-    return ZPush(detail::StageFrame(keys), detail::StageFrame(vals), SVector<int>(), cmd, cb, priority);
+    const bool hbm = servers_take_hbm_.load();
+    return ZPush(detail::StageFrame(keys, hbm), detail::StageFrame(vals, hbm), SVector<int>(), cmd, cb, priority);
   }
 
   /* KVApp.h:148-162 */
   int Pull(const std::vector<Key>& keys, std::vector<Value>* vals, std::vector<int>* lens = nullptr,
            int cmd = 0, const Callback& cb = nullptr, int priority = 0) {
-    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys);
+    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys, servers_take_hbm_.load());
     int ts = AddPullCB(skeys, vals, lens, cmd, cb);
     Data kvs;
     kvs.keys = skeys;
@@ -175,8 +181,9 @@ class KVWorker : public SimpleApp {
       outs->resize(vals.size());
     else
       CHECK_EQ(vals.size(), outs->size());
-    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys);
-    SVector<Value> svals = lens ? SVector<Value>(vals) : detail::StageFrame(vals);
+    const bool hbm = servers_take_hbm_.load();
+    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys, hbm);
+    SVector<Value> svals = lens ? SVector<Value>(vals) : detail::StageFrame(vals, hbm);
     auto souts = new SVector<Value>(outs->data(), outs->size());
     SVector<int>* slens = lens ? new SVector<int>(lens->data(), lens->size()) : nullptr;
     return ZPushPull(skeys, svals, souts, slens, cmd,
@@ -235,6 +242,20 @@ class KVWorker : public SimpleApp {
     Data kv;
     int sender;
   };
+  // servers whose replies said their handle takes HBM frames
+  void NoteHbmServer(int sender) {
+    std::lock_guard<std::mutex> lk(mu_);
+    const int ns = PostOffice::Get()->num_servers();
+    if (hbm_server_.size() != (size_t)ns) hbm_server_.assign(ns, 0);
+    const int r = PostOffice::IDToRank(sender);
+    if (r < ns && !hbm_server_[r]) {
+      hbm_server_[r] = 1;
+      if (++hbm_count_ == ns) servers_take_hbm_ = true;
+    }
+  }
+  std::vector<char> hbm_server_;
+  int hbm_count_ = 0;
+  std::atomic<bool> servers_take_hbm_{false};
 
   void AddCallback(int timestamp, const Callback& cb) {
     if (!cb) return;
@@ -299,7 +320,7 @@ class KVServer : public SimpleApp {
   // handle (it is created with the KVServer); it waits for the handle instead
   // of failing the reference's CHECK (KVApp.h:487) on that race.
   ReqHandle request_handle_;
-  bool device_frames_ = false;
+  std::atomic<bool> device_frames_{false};
   std::mutex handle_mu_;
   std::condition_variable handle_cv_;
 };
@@ -488,6 +509,8 @@ void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
   msg.meta.head = req.cmd;
   msg.meta.timestamp = req.timestamp;
   msg.meta.receiver = req.sender;
+  // tells the worker that HBM frames reach this handle without a copy back
+  msg.meta.hbm_handle = device_frames_.load();
   if (res.keys.size()) {
     msg.AddData(res.keys);
     msg.AddData(res.vals);
@@ -600,6 +623,7 @@ void KVWorker<Value>::OnReceive(const Message& msg) {
     return;
   }
   const int ts = msg.meta.timestamp;
+  if (msg.meta.hbm_handle && !servers_take_hbm_.load()) NoteHbmServer(msg.meta.sender);
   if (msg.meta.pull) {
     CHECK_GE(msg.data.size(), (size_t)2);
     Reply r;

@@ -2,8 +2,10 @@
 //
 // Workers hold keys and values either in HBM (ZPush / ZPull on device
 // SVectors: device slicer, frames read in place by the server kernels, pull
-// replies merged by psg_merge) or in host std::vectors (Push / Pull: frames
-// staged into HBM by the server handle, replies copied back).  The servers run
+// replies merged by psg_merge) or in host std::vectors (Push / Pull: the
+// worker stages them into HBM once the servers have said their handle takes
+// HBM frames — the untimed first requests go as host frames — and copies the
+// merged reply back).  The servers run
 // KVServerDefaultHandle<float> (HBM store).  Checks the test_kv_app.cpp
 // expectations (50 pushes -> 50 * vals, 50 push-pulls -> 100 * vals) and
 // prints one JSON line of timings per worker:
