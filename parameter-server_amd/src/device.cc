@@ -182,14 +182,27 @@ void CopySync(void* dst, const void* src, size_t bytes, int kind) {
 
 namespace {
 // Two pinned staging blocks per thread and the events that tell when the DMA
-// out of / into each one is done.  Kept for the thread's life (like its stream).
+// out of / into each one is done.  A thread that ends hands them to a global
+// free list (no HIP call at thread exit, which may come after the runtime's
+// teardown), and the next thread that stages takes them from there.
 constexpr size_t kStageChunk = size_t(16) << 20;
-struct Staging {
+struct StagePair {
   void* block[2] = {nullptr, nullptr};
   psg_event done[2] = {nullptr, nullptr};
+};
+std::mutex g_stage_mu;
+std::vector<StagePair>* g_stage_free = new std::vector<StagePair>();  // never destroyed
+
+struct Staging {
+  StagePair p;
   bool pending[2] = {false, false};
   bool ok = false;
   bool tried = false;
+  ~Staging() {
+    if (!ok) return;
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    g_stage_free->push_back(p);
+  }
 };
 thread_local Staging t_stage;
 
@@ -197,9 +210,19 @@ Staging* GetStaging() {
   Staging& st = t_stage;
   if (!st.tried) {
     st.tried = true;
-    st.ok = true;
-    for (int b = 0; b < 2 && st.ok; ++b)
-      st.ok = psg_host_alloc(&st.block[b], kStageChunk) == PSG_OK && psg_event_create(&st.done[b]) == PSG_OK;
+    {
+      std::lock_guard<std::mutex> lk(g_stage_mu);
+      if (!g_stage_free->empty()) {
+        st.p = g_stage_free->back();
+        g_stage_free->pop_back();
+        st.ok = true;
+      }
+    }
+    if (!st.ok) {
+      st.ok = true;
+      for (int b = 0; b < 2 && st.ok; ++b)
+        st.ok = psg_host_alloc(&st.p.block[b], kStageChunk) == PSG_OK && psg_event_create(&st.p.done[b]) == PSG_OK;
+    }
   }
   return st.ok ? &st : nullptr;
 }
@@ -216,10 +239,10 @@ void StageToDevice(void* dst_dev, const void* src_host, size_t bytes) {
   int b = 0;
   for (size_t off = 0; off < bytes; off += kStageChunk, b ^= 1) {
     const size_t len = std::min(kStageChunk, bytes - off);
-    if (st->pending[b]) Check(psg_event_sync(st->done[b]), "psg_event_sync");  // block b's last DMA
-    HostCopy(st->block[b], (const char*)src_host + off, len);
-    Check(psg_memcpy((char*)dst_dev + off, st->block[b], len, 0, s), "psg_memcpy H2D");
-    Check(psg_event_record(st->done[b], s), "psg_event_record");
+    if (st->pending[b]) Check(psg_event_sync(st->p.done[b]), "psg_event_sync");  // block b's last DMA
+    HostCopy(st->p.block[b], (const char*)src_host + off, len);
+    Check(psg_memcpy((char*)dst_dev + off, st->p.block[b], len, 0, s), "psg_memcpy H2D");
+    Check(psg_event_record(st->p.done[b], s), "psg_event_record");
     st->pending[b] = true;
   }
   Check(psg_stream_sync(s), "psg_stream_sync");
@@ -237,16 +260,16 @@ void StageToHost(void* dst_host, const void* src_dev, size_t bytes) {
   const size_t n = (bytes + kStageChunk - 1) / kStageChunk;
   auto issue = [&](size_t c) {
     const size_t off = c * kStageChunk, len = std::min(kStageChunk, bytes - off);
-    Check(psg_memcpy(st->block[c & 1], (const char*)src_dev + off, len, 1, s), "psg_memcpy D2H");
-    Check(psg_event_record(st->done[c & 1], s), "psg_event_record");
+    Check(psg_memcpy(st->p.block[c & 1], (const char*)src_dev + off, len, 1, s), "psg_memcpy D2H");
+    Check(psg_event_record(st->p.done[c & 1], s), "psg_event_record");
   };
   issue(0);
   for (size_t c = 0; c < n; ++c) {
     // chunk c + 1 goes on PCIe while chunk c is copied out of its block
     if (c + 1 < n) issue(c + 1);
-    Check(psg_event_sync(st->done[c & 1]), "psg_event_sync");
+    Check(psg_event_sync(st->p.done[c & 1]), "psg_event_sync");
     const size_t off = c * kStageChunk, len = std::min(kStageChunk, bytes - off);
-    HostCopy((char*)dst_host + off, st->block[c & 1], len);
+    HostCopy((char*)dst_host + off, st->p.block[c & 1], len);
   }
   st->pending[0] = st->pending[1] = false;
 }
