@@ -110,6 +110,23 @@ def test_device_frames_end_to_end(ns, nw):
     assert len(lines) == nw
 
 
+@pytest.mark.parametrize("procs", [False, True])
+def test_host_vectors_staged_into_hbm(procs):
+    """Host-vector Push / Pull / PushPull of arrays past the 4 MiB staging
+    threshold (1.2 M keys: 9.6 MB of keys, 4.8 MB of values) over two servers:
+    after the first replies carry the hbm_handle bit, the worker stages its
+    vectors into HBM (pipelined chunks), the device slicer cuts them, and the
+    merged Pull replies come back through the pinned blocks; the harness checks
+    every value (test_kv_app.cpp's expectations)."""
+    exe = os.path.join(BIN, "kv_cluster_device")
+    _need(exe)
+    args = ["-ns", 2, "-nw", 2] + (["-procs"] if procs else []) + [1200000, 3]
+    r = run(exe, *args)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 2
+
+
 # ---- process mode: one node per OS process (src/tcp_van.cc) -------------------
 # The launcher's -procs does what tests/local.py does: a scheduler, ns servers
 # and nw workers as separate processes that meet over TCP.  Host frames travel
