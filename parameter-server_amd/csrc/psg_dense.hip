@@ -17,6 +17,7 @@
 // Measured HBM traffic of the Push kernel = 1.00003 x the 12 B/elem algorithmic
 // bytes (profiles/pmc_push_traffic.json): no re-reads.
 #include <cstdlib>
+#include <type_traits>
 
 #include "psg_internal.h"
 
@@ -348,21 +349,35 @@ static int run_slots(int op, void* store, const uint32_t* slots, const void* val
     const uint64_t nq = (aligned16(slots) && (!need_vals || aligned16(vals)) && (!need_out || aligned16(out)))
                             ? n / 4 : 0;
     if (nq) {
-      constexpr int U = 2;
-      const unsigned g = stream_grid(nq, (uint64_t)kBlock * U, 4);
-      switch (op) {
-        case PSG_PUSH:
-          k_slots_vec<DT, PSG_PUSH, U><<<g, kBlock, 0, s>>>((T*)store, (const u32x4*)slots, (const u32x4*)vals,
-                                                            (u32x4*)out, nq);
-          break;
-        case PSG_PULL:
-          k_slots_vec<DT, PSG_PULL, U><<<g, kBlock, 0, s>>>((T*)store, (const u32x4*)slots, (const u32x4*)vals,
-                                                            (u32x4*)out, nq);
-          break;
-        default:
-          k_slots_vec<DT, PSG_PUSH | PSG_PULL, U><<<g, kBlock, 0, s>>>(
-              (T*)store, (const u32x4*)slots, (const u32x4*)vals, (u32x4*)out, nq);
-      }
+      // one group of four per lane at 8 blocks/CU: 10 M cached keys, Push+Pull
+      // 1,711 GB/s against 1,689 at 2 groups x 4 blocks/CU (3 runs each);
+      // PSG_SLOTS_U / PSG_SLOTS_BPC override it for sweeps
+      static const int su = [] { const char* e = getenv("PSG_SLOTS_U"); return e ? atoi(e) : 1; }();
+      static const int sb = [] {
+        const char* e = getenv("PSG_SLOTS_BPC");
+        const int v = e ? atoi(e) : 8;
+        return v >= 1 && v <= 32 ? v : 8;
+      }();
+      auto go = [&](auto uc) {
+        constexpr int U = decltype(uc)::value;
+        const unsigned g = stream_grid(nq, (uint64_t)kBlock * U, sb);
+        switch (op) {
+          case PSG_PUSH:
+            k_slots_vec<DT, PSG_PUSH, U><<<g, kBlock, 0, s>>>((T*)store, (const u32x4*)slots, (const u32x4*)vals,
+                                                              (u32x4*)out, nq);
+            break;
+          case PSG_PULL:
+            k_slots_vec<DT, PSG_PULL, U><<<g, kBlock, 0, s>>>((T*)store, (const u32x4*)slots, (const u32x4*)vals,
+                                                              (u32x4*)out, nq);
+            break;
+          default:
+            k_slots_vec<DT, PSG_PUSH | PSG_PULL, U><<<g, kBlock, 0, s>>>(
+                (T*)store, (const u32x4*)slots, (const u32x4*)vals, (u32x4*)out, nq);
+        }
+      };
+      if (su == 1) go(std::integral_constant<int, 1>());
+      else if (su == 4) go(std::integral_constant<int, 4>());
+      else go(std::integral_constant<int, 2>());
       PSG_HIP(hipGetLastError());
       const uint64_t done = nq * 4;
       if (done == n) return PSG_OK;
