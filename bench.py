@@ -126,7 +126,19 @@ class GpuBackend:
                                  "(PSG_BENCH_SHARE_GPU has no keyed path)")
             if not self.share_gpu:
                 uid = self.group.broadcast(p.comm_id() if self.rank == 0 else None)
-                self.comm = p.Comm(uid, self.world, self.rank)
+                try:
+                    self.comm = p.Comm(uid, self.world, self.rank)
+                except Exception as e:  # noqa: BLE001
+                    print(f"rank {self.rank}: RCCL init failed ({e})", file=sys.stderr)
+                    self.comm = None
+                # every rank agrees: without a communicator on all of them the
+                # exchange is the xGMI kernels alone
+                if not all(self.group.all_gather(self.comm is not None)):
+                    if self.comm is not None:
+                        self.comm.close()
+                    self.comm = None
+                    if self.keyed:
+                        raise SystemExit("the keyed N > 1 exchange needs RCCL, which failed to start")
             self.scratch = p.DeviceBuffer(blk * self.vb)
             if not self.keyed:
                 self._setup_xgmi()
