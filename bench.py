@@ -163,7 +163,7 @@ class GpuBackend:
         self._peer_ptrs = []
         sptr = self.store.info().vals
         try:
-            mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr))
+            mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr), p.ipc_export(self.out.ptr))
         except Exception as e:  # noqa: BLE001
             print(f"rank {self.rank}: hipIpc export unavailable ({e}); xGMI exchange off",
                   file=sys.stderr)
@@ -172,18 +172,22 @@ class GpuBackend:
         if any(h is None for h in allh):
             return
         tag = self.group.broadcast(uuid.uuid4().hex[:16] if self.rank == 0 else None)
-        vptrs, sptrs, ok = [], [], True
+        vptrs, sptrs, optrs, ok = [], [], [], True
         try:
             for r in range(self.world):
                 if r == self.rank:
                     vptrs.append(self.vals.ptr)
                     sptrs.append(sptr)
+                    optrs.append(self.out.ptr)
                 else:
                     vptrs.append(p.ipc_open(allh[r][0]))
                     self._peer_ptrs.append(vptrs[-1])
                     sptrs.append(p.ipc_open(allh[r][1]))
                     self._peer_ptrs.append(sptrs[-1])
+                    optrs.append(p.ipc_open(allh[r][2]))
+                    self._peer_ptrs.append(optrs[-1])
             x = p.Xgmi(self.world, self.rank, vptrs, sptrs)
+            x.set_outs(optrs)
             b = p.NodeBarrier("psg_bench_" + tag, self.world, self.rank)
         except Exception as e:  # noqa: BLE001
             print(f"rank {self.rank}: xGMI mapping failed ({e}); xGMI exchange off", file=sys.stderr)
@@ -259,6 +263,11 @@ class GpuBackend:
             self.stream.sync()
             self.node_barrier.wait()
             return
+        if self.mode == "xgmiw":
+            # the write form needs no barrier between the phases: the Pull
+            # writes this rank's own shard out once its own Push is done
+            self.xgmi.push(self.store, self.L, self.stream)
+            return
         if self.cached:
             self.store.handle_slots(self.p.PUSH, self.slots, self.vals, None, self.L, stream=self.stream)
         elif self.keyed:
@@ -286,6 +295,13 @@ class GpuBackend:
             self.stream.sync()
             self.node_barrier.wait()
             return
+        if self.mode == "xgmiw":
+            # every rank writes its shard into every output; an output is
+            # complete when all ranks' writes are (sync, then one barrier)
+            self.xgmi.pull_write(self.store, self.L, self.stream)
+            self.stream.sync()
+            self.node_barrier.wait()
+            return
         if self.cached:
             self.store.handle_slots(self.p.PULL, self.slots, None, self.out, self.L, stream=self.stream)
         elif self.keyed:
@@ -303,6 +319,9 @@ class GpuBackend:
     def step(self):
         if self.mode == "xgmi":
             self._xgmi_double_buffered_step()
+            return
+        if self.mode == "xgmiw":
+            self._xgmi_write_step()
             return
         self.comm.push_pull(self.store, self.vals, self.out, self.L, self.nbuckets, self.stream)
 
@@ -332,6 +351,31 @@ class GpuBackend:
         self.stream2.sync()
         self.node_barrier.wait()
 
+    def _xgmi_write_step(self):
+        """The write form double-buffered: chunk c's Push (reads the peers:
+        ingress) on the main stream; chunk c's Pull as writes (egress) on a
+        second stream once this rank's own Push of chunk c is done (an event,
+        no barrier), so the two directions of every xGMI link carry the two
+        phases at once.  One barrier per step, after both streams drain."""
+        p = self.p
+        if getattr(self, "stream2", None) is None:
+            self.stream2 = p.Stream()
+        unit = 16 // self.vb
+        chunk = ((self.blk + self.nbuckets - 1) // self.nbuckets + unit - 1) // unit * unit
+        bounds = [(off, min(chunk, self.blk - off)) for off in range(0, self.blk, chunk)]
+        evs = getattr(self, "_db_events", [])
+        while len(evs) < len(bounds):
+            evs.append(p.Event())
+        self._db_events = evs
+        for i, (off, cnt) in enumerate(bounds):
+            self.xgmi.push_range(self.store, self.L, off, cnt, self.stream)
+            evs[i].record(self.stream)
+            self.stream2.wait(evs[i])
+            self.xgmi.pull_write_range(self.store, self.L, off, cnt, self.stream2)
+        self.stream2.sync()
+        self.stream.sync()
+        self.node_barrier.wait()
+
     def _set_mode(self, cand):
         mode, nb = cand
         self.mode, self.nbuckets = mode, nb
@@ -346,17 +390,18 @@ class GpuBackend:
         if self.world == 1 or self.keyed:
             return
         cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
+        two_stream = [("xgmi", 2), ("xgmi", 4), ("xgmiw", 2), ("xgmiw", 4)]
         if self.xgmi is not None:
-            cands.append(("xgmi", 0))
-            # the double-buffered step adds a second stream per rank; with every
+            cands += [("xgmi", 0), ("xgmiw", 0)]
+            # the double-buffered steps add a second stream per rank; with every
             # rank on ONE GPU (test mode) that oversubscribes the hardware queues
             # and slows every later step ~4x (measured at N = 8), so test mode
-            # times it only when forced
+            # times them only when forced
             if not self.share_gpu:
-                cands += [("xgmi", 2), ("xgmi", 4)]
-        forced = os.environ.get("PSG_BENCH_EXCHANGE")  # testing: e.g. "xgmi/4", "rccl/1"
+                cands += two_stream
+        forced = os.environ.get("PSG_BENCH_EXCHANGE")  # testing: e.g. "xgmi/4", "xgmiw/2", "rccl/1"
         if forced and self.xgmi is not None:
-            cands += [c for c in (("xgmi", 2), ("xgmi", 4)) if c not in cands]
+            cands += [c for c in two_stream if c not in cands]
         if forced:
             m, _, nb = forced.partition("/")
             cands = [c for c in cands if c == (m, int(nb or 0))]
@@ -380,11 +425,11 @@ class GpuBackend:
         self.calibration = {f"{m}{'' if nb == 0 else '/' + str(nb)}": round(x, 4)
                             for (m, nb), x in zip(cands, t)}
         self.pushes_in_calibration = len(cands) * (iters + 1)
-        if self.mode == "xgmi":
+        if self.mode in ("xgmi", "xgmiw"):
             self.pushes_in_calibration += 1
             self.exchange_verified = self._verify_xgmi()
             if not self.exchange_verified:
-                rest = [cands[i] for i in order if cands[i][0] != "xgmi"]
+                rest = [cands[i] for i in order if not cands[i][0].startswith("xgmi")]
                 if not rest:
                     raise RuntimeError("xGMI exchange failed its checksum verification "
                                        "and no RCCL communicator is available")
@@ -434,7 +479,7 @@ class GpuBackend:
         a, b = self.new_event(), self.new_event()
         self.record(a)
         for _ in range(iters):
-            if self.mode == "xgmi":
+            if self.mode in ("xgmi", "xgmiw"):
                 # reads the peers' (constant) request vectors and writes only this
                 # rank's shard: safe to repeat without a barrier
                 self.xgmi.push(self.store, self.L, self.stream)
@@ -447,7 +492,7 @@ class GpuBackend:
 
     def probe_kernel(self):
         """(name, algorithmic bytes per launch) of the kernel accumulate_probe times."""
-        if self.mode == "xgmi":
+        if self.mode in ("xgmi", "xgmiw"):
             # store read + write (8 B) + one 4-B value from every rank's vector
             return ("k_xgmi_push (fused reduce of %d ranks' blocks + accumulate; "
                     "%d of them read over xGMI)" % (self.world, self.world - 1),
@@ -675,6 +720,13 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                                          "second HIP stream while chunk c+1's Push runs" % backend.nbuckets)
         elif getattr(backend, "mode", "rccl") == "xgmi":
             res["config"]["exchange"] = "one-shot xGMI kernels (psg_xgmi push/pull, peers via hipIpc)"
+        elif getattr(backend, "mode", "rccl") == "xgmiw" and fused:
+            res["config"]["exchange"] = ("xGMI Push (reads the peers) with the Pull as writes into every "
+                                         "rank's output, double-buffered over %d chunks on two HIP streams: "
+                                         "the two directions of each link at once" % backend.nbuckets)
+        elif getattr(backend, "mode", "rccl") == "xgmiw":
+            res["config"]["exchange"] = ("xGMI Push (reads the peers) then the Pull as writes into every "
+                                         "rank's output (psg_xgmi_pull_write); one barrier per step")
         elif getattr(backend, "mode", "") == "xgmi-keyed":
             res["config"]["exchange"] = ("keyed xGMI kernels on cached slots (psg_xgmi_push_slots / "
                                          "_pull_slots over the peers' values, stores and slot lists)")

@@ -115,6 +115,8 @@ int psg_event_destroy(psg_event ev);
 int psg_event_record(psg_event ev, psg_stream stream);
 int psg_event_sync(psg_event ev);
 int psg_event_elapsed_ms(psg_event start, psg_event stop, float* ms);
+/* later work on `stream` waits for `ev` (recorded on another stream) */
+int psg_stream_wait_event(psg_stream stream, psg_event ev);
 
 /* Seeded synthetic data generated on the device: element i of the output is a
  * pure function of (seed, i), so the CPU oracle regenerates it bit-exactly
@@ -317,6 +319,21 @@ int psg_xgmi_push_range(psg_xgmi* x, psg_store* shard, uint64_t n_total, uint64_
                         uint64_t cnt, psg_stream stream);
 int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total,
                         uint64_t off, uint64_t cnt, psg_stream stream);
+/* The Pull as writes (egress) instead of reads (ingress).  psg_xgmi_set_outs
+ * registers every rank's Pull output buffer (n_total values, mapped here;
+ * this rank's own at [rank]).  psg_xgmi_pull_write_range then copies this
+ * rank's shard elements [off, off + cnt) into out_w[rank * blk + off ...] of
+ * every rank w: the all-gather pushed out over the links while the Push
+ * (psg_xgmi_push*, which reads its peers) uses the other direction of each
+ * full-duplex link.  It needs only this rank's own Push of that range to be
+ * complete (stream order): no barrier between the phases.  A rank's output
+ * is complete once every rank's writes are: the caller synchronises its
+ * stream and passes a psg_node_barrier before any rank reads its output, and
+ * before the next step's writes. */
+int psg_xgmi_set_outs(psg_xgmi* x, void* const* peer_outs);
+int psg_xgmi_pull_write_range(psg_xgmi* x, psg_store* shard, uint64_t n_total, uint64_t off,
+                              uint64_t cnt, psg_stream stream);
+int psg_xgmi_pull_write(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream);
 /* Keyed exchange on cached slots (configs[3] with LR key caching): every rank
  * pushes values for the SAME key list; [seg_off, seg_off + seg_n) is the
  * psg_slice segment of this rank's shard, and `slots` its psg_store_resolve

@@ -306,6 +306,12 @@ int psg_event_elapsed_ms(psg_event start, psg_event stop, float* ms) {
   return PSG_OK;
 }
 
+int psg_stream_wait_event(psg_stream stream, psg_event ev) {
+  PSG_REQUIRE(ev, PSG_ERR_INVALID, "psg_stream_wait_event: null event");
+  PSG_HIP(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0));
+  return PSG_OK;
+}
+
 int psg_fill_synth(void* dptr, uint64_t n, int dtype, uint64_t seed, int mode, double lo,
                    double hi, psg_stream stream) {
   if (n == 0) return PSG_OK;

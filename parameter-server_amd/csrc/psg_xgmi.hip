@@ -13,6 +13,9 @@
 //                         one pass over HBM.
 //   Pull (psg_xgmi_pull)  rank r:  out[w*blk + i] = shard_w[i] for every w —
 //                         the all-gather, reading N-1 peers' shards in place.
+//   Pull as writes (psg_xgmi_pull_write)  rank r:  out_w[r*blk + i] = shard[i]
+//                         for every w — the same all-gather pushed out over
+//                         the links (egress) while the Push reads (ingress).
 //
 // Ordering between ranks is the caller's: all Pushes must be complete before
 // any Pull reads a shard, and every Pull complete before the next Push
@@ -81,6 +84,37 @@ __global__ __launch_bounds__(256) void k_xgmi_pull(u32x4* __restrict__ out, Peer
     for (int u = 0; u < kPullU; ++u) {
       const uint64_t j = base + (uint64_t)u * kBlock;
       if (j < nvec) __builtin_nontemporal_store(v[u], o + j);
+    }
+  }
+}
+
+// The Pull as writes: v = shard[j] (local HBM, read once), then one
+// non-temporal 16-B store of v into every rank's output (remote stores over
+// xGMI are posted: no round trip per access, unlike the reads of k_xgmi_pull).
+// Two vectors per lane in flight.
+struct Outs {
+  u32x4* p[kMaxPeers];
+};
+constexpr int kScatterU = 2;
+__global__ __launch_bounds__(256) void k_xgmi_scatter(const u32x4* __restrict__ shard, Outs outs, int nout,
+                                                      uint64_t nvec) {
+  const uint64_t tile = (uint64_t)kBlock * kScatterU;
+  for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec;
+       base += (uint64_t)gridDim.x * tile) {
+    u32x4 v[kScatterU];
+#pragma unroll
+    for (int u = 0; u < kScatterU; ++u) {
+      const uint64_t j = base + (uint64_t)u * kBlock;
+      if (j < nvec) v[u] = __builtin_nontemporal_load(shard + j);
+    }
+#pragma unroll
+    for (int w = 0; w < kMaxPeers; ++w) {
+      if (w >= nout) break;
+#pragma unroll
+      for (int u = 0; u < kScatterU; ++u) {
+        const uint64_t j = base + (uint64_t)u * kBlock;
+        if (j < nvec) __builtin_nontemporal_store(v[u], outs.p[w] + j);
+      }
     }
   }
 }
@@ -163,6 +197,7 @@ struct psg_xgmi {
   int nranks, rank;
   void* vals[psg::kMaxPeers];
   void* stores[psg::kMaxPeers];
+  void* outs[psg::kMaxPeers];  // psg_xgmi_set_outs (the write form of the Pull)
 };
 
 struct psg_barrier {
@@ -391,6 +426,51 @@ int psg_xgmi_pull_range(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_tot
 int psg_xgmi_pull(psg_xgmi* x, psg_store* shard, void* out, uint64_t n_total, psg_stream stream) {
   PSG_REQUIRE(x && shard, PSG_ERR_INVALID, "psg_xgmi_pull: null argument");
   return psg_xgmi_pull_range(x, shard, out, n_total, 0, n_total / (uint64_t)x->nranks, stream);
+}
+
+int psg_xgmi_set_outs(psg_xgmi* x, void* const* peer_outs) {
+  PSG_REQUIRE(x && peer_outs, PSG_ERR_INVALID, "psg_xgmi_set_outs: null argument");
+  for (int r = 0; r < x->nranks; ++r) {
+    PSG_REQUIRE(peer_outs[r] && aligned16(peer_outs[r]), PSG_ERR_INVALID,
+                "psg_xgmi_set_outs: output %d null or not 16-B aligned", r);
+    x->outs[r] = peer_outs[r];
+  }
+  return PSG_OK;
+}
+
+int psg_xgmi_pull_write_range(psg_xgmi* x, psg_store* shard, uint64_t n_total, uint64_t off, uint64_t cnt,
+                              psg_stream stream) {
+  PSG_REQUIRE(x && shard && shard->kind == PSG_STORE_DENSE, PSG_ERR_INVALID,
+              "psg_xgmi_pull_write: need a DENSE shard");
+  PSG_REQUIRE(x->outs[0] != nullptr, PSG_ERR_INVALID, "psg_xgmi_pull_write: no outputs (psg_xgmi_set_outs)");
+  PSG_REQUIRE(n_total % (uint64_t)x->nranks == 0, PSG_ERR_INVALID, "psg_xgmi_pull_write: n_total %% nranks");
+  const int es = shard->esize;
+  const uint64_t blk = n_total / (uint64_t)x->nranks;
+  PSG_REQUIRE(shard->capacity >= blk, PSG_ERR_RANGE, "psg_xgmi_pull_write: shard too small");
+  PSG_REQUIRE(shard->vals == x->stores[x->rank], PSG_ERR_INVALID,
+              "psg_xgmi_pull_write: shard is not this rank's store");
+  PSG_REQUIRE(off <= blk && cnt <= blk - off, PSG_ERR_RANGE,
+              "psg_xgmi_pull_write: range [%llu, +%llu) outside the block", (unsigned long long)off,
+              (unsigned long long)cnt);
+  PSG_REQUIRE((blk * es) % 16 == 0 && (off * es) % 16 == 0 && (cnt * es) % 16 == 0, PSG_ERR_INVALID,
+              "psg_xgmi_pull_write: block, offset and count must be multiples of 16 B");
+  const uint64_t nvec = cnt * es / 16;
+  if (nvec == 0) return PSG_OK;
+  Outs o;
+  for (int w = 0; w < x->nranks; ++w)
+    o.p[w] = (u32x4*)((char*)x->outs[w] + ((uint64_t)x->rank * blk + off) * es);
+  uint64_t g = (nvec + (uint64_t)kBlock * kScatterU - 1) / ((uint64_t)kBlock * kScatterU);
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 4;  // 2 per CU
+  if (g > cap) g = cap;
+  k_xgmi_scatter<<<(unsigned)g, kBlock, 0, (hipStream_t)stream>>>(
+      (const u32x4*)((const char*)shard->vals + off * es), o, x->nranks, nvec);
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int psg_xgmi_pull_write(psg_xgmi* x, psg_store* shard, uint64_t n_total, psg_stream stream) {
+  PSG_REQUIRE(x && shard, PSG_ERR_INVALID, "psg_xgmi_pull_write: null argument");
+  return psg_xgmi_pull_write_range(x, shard, n_total, 0, n_total / (uint64_t)x->nranks, stream);
 }
 
 // ---- node barrier: a sense-counting barrier in a POSIX shared-memory page --

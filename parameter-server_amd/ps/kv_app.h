@@ -143,6 +143,7 @@ class KVWorker : public SimpleApp {
     slicer_ = [this](Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced) {
       DefaultSlicer(send, ranges, sliced);
     };
+    app_id_ = app_id;
     customer_ = new Customer(app_id, customer_id, [this](const Message& m) { OnReceive(m); });
   }
   ~KVWorker() override {
@@ -283,6 +284,7 @@ class KVServer : public SimpleApp {
   using ReqHandle = std::function<void(const KVMeta& req_meta, const KVPairs<Value>& req_data, KVServer* server)>;
 
   explicit KVServer(int app_id) : SimpleApp() {
+    app_id_ = app_id;
     customer_ = new Customer(app_id, app_id, [this](const Message& m) { OnReceive(m); });
   }
   ~KVServer() override {

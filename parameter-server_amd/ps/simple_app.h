@@ -1,7 +1,10 @@
 // ps/simple_app.h — head/body request-response app, the base of KVWorker and
 // KVServer (reference src/ps/SimpleApp.{h,cpp}).
 #pragma once
+#include <chrono>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <string>
 
 #include "internal/customer.h"
@@ -36,8 +39,18 @@ class SimpleApp {
   SimpleApp();
   virtual void OnReceive(const Message& msg);
   Customer* customer_{nullptr};
+  int app_id_ = 0;  // known before customer_ is, which may already dispatch
 
  private:
+  // The handles are swapped by the program's thread while the customer thread
+  // may be calling them: guarded.  A request that arrives within the first
+  // second of the app, before the program installed its handle, waits for it
+  // (the program's next statement after the constructor, as in
+  // test_simple_app.cpp) instead of taking the default one.
+  std::mutex handle_mu_;
+  std::condition_variable handle_cv_;
+  bool user_request_handle_ = false;
+  std::chrono::steady_clock::time_point created_ = std::chrono::steady_clock::now();
   Handle request_handle_;
   Handle response_handle_;
 };

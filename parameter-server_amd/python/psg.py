@@ -38,7 +38,7 @@ EXPORTS = [
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
     "psg_memset", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
     "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
-    "psg_event_elapsed_ms", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
+    "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
     "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
@@ -50,7 +50,8 @@ EXPORTS = [
     "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
     "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_xgmi_push_range",
-    "psg_xgmi_pull_range", "psg_xgmi_push_slots", "psg_xgmi_pull_slots", "psg_node_barrier_create",
+    "psg_xgmi_pull_range", "psg_xgmi_set_outs", "psg_xgmi_pull_write_range", "psg_xgmi_pull_write",
+    "psg_xgmi_push_slots", "psg_xgmi_pull_slots", "psg_node_barrier_create",
     "psg_node_barrier_wait", "psg_node_barrier_destroy",
 ]
 
@@ -97,6 +98,7 @@ def lib() -> C.CDLL:
             "psg_event_destroy": ([vp], i32), "psg_event_record": ([vp, vp], i32),
             "psg_event_sync": ([vp], i32),
             "psg_event_elapsed_ms": ([vp, vp, C.POINTER(f32)], i32),
+            "psg_stream_wait_event": ([vp, vp], i32),
             "psg_fill_synth": ([vp, u64, i32, u64, i32, f64, f64, vp], i32),
             "psg_fill_keys_arith": ([vp, u64, u64, u64, vp], i32),
             "psg_checksum": ([vp, u64, C.POINTER(u64), vp], i32),
@@ -137,6 +139,9 @@ def lib() -> C.CDLL:
             "psg_xgmi_pull": ([vp, vp, vp, u64, vp], i32),
             "psg_xgmi_push_range": ([vp, vp, u64, u64, u64, vp], i32),
             "psg_xgmi_pull_range": ([vp, vp, vp, u64, u64, u64, vp], i32),
+            "psg_xgmi_set_outs": ([vp, C.POINTER(vp)], i32),
+            "psg_xgmi_pull_write_range": ([vp, vp, u64, u64, u64, vp], i32),
+            "psg_xgmi_pull_write": ([vp, vp, u64, vp], i32),
             "psg_xgmi_push_slots": ([vp, vp, vp, u64, u64, vp], i32),
             "psg_xgmi_pull_slots": ([vp, vp, C.POINTER(vp), vp, vp, vp, vp], i32),
             "psg_node_barrier_create": ([C.c_char_p, i32, i32, C.POINTER(vp)], i32),
@@ -196,6 +201,10 @@ class Stream:
 
     def sync(self) -> None:
         _call("psg_stream_sync", self.handle)
+
+    def wait(self, ev: "Event") -> None:
+        """Later work on this stream waits for `ev`."""
+        _call("psg_stream_wait_event", self.handle, ev.handle)
 
     def close(self) -> None:
         if self.handle.value:
@@ -502,6 +511,17 @@ class Xgmi:
 
     def pull_range(self, shard: Store, out, n_total: int, off: int, cnt: int, stream=None) -> None:
         _call("psg_xgmi_pull_range", self.h, shard.h, _ptr(out), n_total, off, cnt, _s(stream))
+
+    def set_outs(self, out_ptrs) -> None:
+        """Every rank's Pull output buffer, mapped here (own rank: local pointer)."""
+        O = (C.c_void_p * len(out_ptrs))(*[_ptr(p) for p in out_ptrs])
+        _call("psg_xgmi_set_outs", self.h, O)
+
+    def pull_write(self, shard: Store, n_total: int, stream=None) -> None:
+        _call("psg_xgmi_pull_write", self.h, shard.h, n_total, _s(stream))
+
+    def pull_write_range(self, shard: Store, n_total: int, off: int, cnt: int, stream=None) -> None:
+        _call("psg_xgmi_pull_write_range", self.h, shard.h, n_total, off, cnt, _s(stream))
 
     def push_slots(self, shard: Store, slots, seg_off: int, seg_n: int, stream=None) -> None:
         _call("psg_xgmi_push_slots", self.h, shard.h, _ptr(slots), seg_off, seg_n, _s(stream))

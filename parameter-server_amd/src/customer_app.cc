@@ -114,6 +114,7 @@ SimpleApp::SimpleApp() {
 }
 
 SimpleApp::SimpleApp(int app_id, int customer_id) : SimpleApp() {
+  app_id_ = app_id;
   customer_ = new Customer(app_id, customer_id, [this](const Message& m) { OnReceive(m); });
 }
 
@@ -145,7 +146,7 @@ void SimpleApp::Response(const SimpleData& req, const std::string& response_body
   msg.meta.body = response_body;
   msg.meta.request = false;
   msg.meta.simple_app = true;
-  msg.meta.app_id = customer_->app_id();
+  msg.meta.app_id = app_id_;
   msg.meta.customer_id = req.customer_id;
   msg.meta.timestamp = req.request_id;
   msg.meta.receiver = req.sender;
@@ -156,19 +157,29 @@ void SimpleApp::Wait(int request_id) { customer_->WaitRequest(request_id); }
 
 void SimpleApp::SetRequestHandle(const Handle& h) {
   CHECK(static_cast<bool>(h)) << "Handle shouldn't be empty";
-  request_handle_ = h;
+  {
+    std::lock_guard<std::mutex> lk(handle_mu_);
+    request_handle_ = h;
+    user_request_handle_ = true;
+  }
+  handle_cv_.notify_all();
 }
 void SimpleApp::SetResponseHandle(const Handle& h) {
   CHECK(static_cast<bool>(h)) << "Handle shouldn't be empty";
+  std::lock_guard<std::mutex> lk(handle_mu_);
   response_handle_ = h;
 }
 
 void SimpleApp::OnReceive(const Message& msg) {
   SimpleData received{msg.meta.head, msg.meta.sender, msg.meta.customer_id, msg.meta.timestamp, msg.meta.body};
-  if (msg.meta.request)
-    request_handle_(this, received);
-  else
-    response_handle_(this, received);
+  Handle h;
+  {
+    std::unique_lock<std::mutex> lk(handle_mu_);
+    if (msg.meta.request && !user_request_handle_)
+      handle_cv_.wait_until(lk, created_ + std::chrono::seconds(1), [this] { return user_request_handle_; });
+    h = msg.meta.request ? request_handle_ : response_handle_;
+  }
+  h(this, received);
 }
 
 }  // namespace ps

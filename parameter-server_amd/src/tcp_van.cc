@@ -38,6 +38,8 @@
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
+#include <csignal>
+#include <execinfo.h>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -1052,9 +1054,24 @@ const char* RoleOf(int argc, char** argv) {
   return nullptr;
 }
 
+// A node process that faults prints where (addresses; addr2line resolves
+// them against the binary) before it dies, so a crash in a multi-process job
+// names its frame instead of surfacing only as "node N disconnected".
+static void FatalSignal(int sig) {
+  char msg[64];
+  const int n = std::snprintf(msg, sizeof(msg), "[node %d] fatal signal %d; backtrace:\n", (int)getpid(), sig);
+  if (n > 0) (void)!::write(2, msg, (size_t)n);
+  void* frames[48];
+  const int k = ::backtrace(frames, 48);
+  ::backtrace_symbols_fd(frames, k, 2);
+  ::signal(sig, SIG_DFL);
+  ::raise(sig);
+}
+
 int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** argv) {
   const char* role = RoleOf(argc, argv);
   CHECK(role) << "process mode needs a role (argv[3] or PS_ROLE)";
+  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL}) ::signal(sig, FatalSignal);
   ReadLocalConfigToEnv(argv[1]);
   shm::Enable();
   const int ns = Environment::GetIntOrDefault("PS_NUM_SERVER", 1);
@@ -1137,6 +1154,12 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
     if (p > 0) {
       --left;
       const bool bad = !WIFEXITED(status) || WEXITSTATUS(status) != 0;
+      if (WIFSIGNALED(status)) {
+        size_t k = 0;
+        while (k < pids.size() && pids[k] != p) ++k;
+        std::fprintf(stderr, "[launcher] node process %d (%s) killed by signal %d\n", (int)p,
+                     k < logs.size() ? logs[k].c_str() : "?", WTERMSIG(status));
+      }
       if (bad && !rc) {
         rc = 1;
         failed_at = std::chrono::steady_clock::now();

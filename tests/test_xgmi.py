@@ -46,7 +46,7 @@ def test_node_barrier_cpu():
     assert sorted(out.get(timeout=5) for _ in range(3)) == [0, 1, 2]
 
 
-def _xgmi_rank(rank, world, n, steps, name, q_in, q_out, mode=0):
+def _xgmi_rank(rank, world, n, steps, name, q_in, q_out, mode=0, write=False):
     _paths()
     import oracle
     import psg
@@ -59,17 +59,25 @@ def _xgmi_rank(rank, world, n, steps, name, q_in, q_out, mode=0):
     vals.fill_synth(n, psg.F32, 7 + rank, mode, lo_v, hi_v)
     store = psg.Store(psg.DENSE, psg.F32, rank * blk, (rank + 1) * blk, blk)
     sptr = store.info().vals
+    out = psg.DeviceBuffer(n * 4)
     psg.device_sync()
-    q_out.put(("h", rank, psg.ipc_export(vals.ptr), psg.ipc_export(sptr)))
+    q_out.put(("h", rank, psg.ipc_export(vals.ptr), psg.ipc_export(sptr), psg.ipc_export(out.ptr)))
     handles = q_in.get(timeout=120)
     vptrs = [vals.ptr if r == rank else psg.ipc_open(handles[r][0]) for r in range(world)]
     sptrs = [sptr if r == rank else psg.ipc_open(handles[r][1]) for r in range(world)]
+    optrs = [out.ptr if r == rank else psg.ipc_open(handles[r][2]) for r in range(world)]
     x = psg.Xgmi(world, rank, vptrs, sptrs)
+    x.set_outs(optrs)
     bar = psg.NodeBarrier(name, world, rank)
-    out = psg.DeviceBuffer(n * 4)
     bar.wait()
     for _ in range(steps):
         x.push(store, n)
+        if write:
+            # no barrier between the phases: this rank's own Push is done
+            x.pull_write(store, n)
+            psg.device_sync()
+            bar.wait()
+            continue
         psg.device_sync()
         bar.wait()
         x.pull(store, out, n)
@@ -92,13 +100,15 @@ def _xgmi_rank(rank, world, n, steps, name, q_in, q_out, mode=0):
         if r != rank:
             psg.ipc_close(vptrs[r])
             psg.ipc_close(sptrs[r])
+            psg.ipc_close(optrs[r])
     bar.close()
     q_out.put(("r", rank, ok))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,mode", [(2, 0), (3, 0), (2, 1), (3, 1)])
-def test_xgmi_exchange_multiprocess(world, mode):
+@pytest.mark.parametrize("world,mode,write", [(2, 0, False), (3, 0, False), (2, 1, False), (3, 1, False),
+                                              (2, 0, True), (3, 1, True)])
+def test_xgmi_exchange_multiprocess(world, mode, write):
     """Every rank's Push lands on every shard and every Pull reads every shard.
     mode 0: integer-valued data (the reference KATs); mode 1: real-valued
     U(-1, 1).  k_xgmi_push adds the sources to the shard one at a time in rank
@@ -109,14 +119,14 @@ def test_xgmi_exchange_multiprocess(world, mode):
     q_out = ctx.Queue()
     q_in = [ctx.Queue() for _ in range(world)]
     name = "psg_xgmi_" + uuid.uuid4().hex[:12]
-    procs = [ctx.Process(target=_xgmi_rank, args=(r, world, n, 3, name, q_in[r], q_out, mode))
+    procs = [ctx.Process(target=_xgmi_rank, args=(r, world, n, 3, name, q_in[r], q_out, mode, write))
              for r in range(world)]
     for p in procs:
         p.start()
     handles = {}
     for _ in range(world):
-        tag, r, hv, hs = q_out.get(timeout=240)
-        handles[r] = (hv, hs)
+        tag, r, hv, hs, ho = q_out.get(timeout=240)
+        handles[r] = (hv, hs, ho)
     for r in range(world):
         q_in[r].put(handles)
     results = [q_out.get(timeout=240) for _ in range(world)]
@@ -127,11 +137,14 @@ def test_xgmi_exchange_multiprocess(world, mode):
 
 
 @pytest.mark.gpu
-def test_bench_n2_shared_gpu_xgmi_verified():
-    """bench.py's N>1 path end to end with two ranks on one GPU
+@pytest.mark.parametrize("nproc,exchange", [(2, None), (2, "xgmiw/0"), (3, "xgmiw/2")])
+def test_bench_shared_gpu_xgmi_verified(nproc, exchange):
+    """bench.py's N>1 path end to end with its ranks on one GPU
     (PSG_BENCH_SHARE_GPU=1: the xGMI exchange, no RCCL): the calibration's
     checksum verification of the pulled shards must pass and the closed-form
-    parity check must hold after every push the run made."""
+    parity check must hold after every push the run made.  Forced: the Pull as
+    writes (xgmiw/0), and that form double-buffered on two streams over
+    ragged chunks (xgmiw/2 at 3 ranks)."""
     import json
     import socket
     import subprocess
@@ -139,16 +152,21 @@ def test_bench_n2_shared_gpu_xgmi_verified():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = dict(os.environ, PSG_BENCH_SHARE_GPU="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    if exchange:
+        env["PSG_BENCH_EXCHANGE"] = exchange
+    keys = 3 * (1 << 20) + 3 * 4 * 37 if nproc == 3 else 1 << 22
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--keys", str(1 << 22),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--keys", str(keys),
            "--steps", "3", "--warmup", "1"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     res = json.loads(line)
-    assert res["n_gpus"] == 2 and res["parity_check"] is True, res
+    assert res["n_gpus"] == nproc and res["parity_check"] is True, res
     assert res["config"].get("xgmi_checksum_verified") is True, res
+    if exchange:
+        assert "as writes" in res["config"]["exchange"], res["config"]
 
 
 def test_node_barrier_timeout_poisons_and_names_are_exclusive():
