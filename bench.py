@@ -223,23 +223,27 @@ class GpuBackend:
             self.slots = p.DeviceBuffer(4)
         self.sync()
         sptr = self.store.info().vals
-        mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr), p.ipc_export(self.slots.ptr))
+        mine = (p.ipc_export(self.vals.ptr), p.ipc_export(sptr), p.ipc_export(self.slots.ptr),
+                p.ipc_export(self.out.ptr))
         allh = self.group.all_gather(mine)
         tag = self.group.broadcast(uuid.uuid4().hex[:16] if self.rank == 0 else None)
         self._peer_ptrs = []
-        vptrs, sptrs, self.peer_slots = [], [], []
+        vptrs, sptrs, optrs, self.peer_slots = [], [], [], []
         for r in range(self.world):
             if r == self.rank:
                 vptrs.append(self.vals.ptr)
                 sptrs.append(sptr)
                 self.peer_slots.append(self.slots.ptr)
+                optrs.append(self.out.ptr)
             else:
                 opened = [p.ipc_open(h) for h in allh[r]]
                 self._peer_ptrs += opened
                 vptrs.append(opened[0])
                 sptrs.append(opened[1])
                 self.peer_slots.append(opened[2])
+                optrs.append(opened[3])
         self.xgmi = p.Xgmi(self.world, self.rank, vptrs, sptrs)
+        self.xgmi.set_outs(optrs)
         self.node_barrier = p.NodeBarrier("psg_bench_" + tag, self.world, self.rank)
         self.seg_offs = np.array(self.kp[:-1], dtype=np.uint64)
         self.seg_ns = np.array([self.kp[w + 1] - self.kp[w] for w in range(self.world)], dtype=np.uint64)
@@ -257,6 +261,10 @@ class GpuBackend:
             self.xgmi.push_slots(self.store, self.slots, self.seg[0], self.seg[1], self.stream)
             self.stream.sync()
             self.node_barrier.wait()
+            return
+        if self.mode == "xgmi-keyed-w":
+            # the write form: no barrier between the phases (see pull)
+            self.xgmi.push_slots(self.store, self.slots, self.seg[0], self.seg[1], self.stream)
             return
         if self.mode == "xgmi":
             self.xgmi.push(self.store, self.L, self.stream)
@@ -287,6 +295,13 @@ class GpuBackend:
         if self.mode == "xgmi-keyed":
             self.xgmi.pull_slots(self.store, self.peer_slots, self.seg_offs, self.seg_ns, self.out,
                                  self.stream)
+            self.stream.sync()
+            self.node_barrier.wait()
+            return
+        if self.mode == "xgmi-keyed-w":
+            # this rank's segment, read through its own slots, written into every
+            # rank's output; outputs complete after every rank's writes
+            self.xgmi.pull_write_slots(self.store, self.slots, self.seg[0], self.seg[1], self.stream)
             self.stream.sync()
             self.node_barrier.wait()
             return
@@ -387,7 +402,11 @@ class GpuBackend:
         RCCL pipelined over 4/8/16 buckets, or the one-shot xGMI kernels.  The
         max over ranks decides, so every rank picks the same."""
         self.pushes_in_calibration = 0
-        if self.world == 1 or self.keyed:
+        if self.world == 1:
+            return
+        if self.keyed:
+            if self.mode.startswith("xgmi-keyed"):
+                self._calibrate_keyed(iters)
             return
         cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
         two_stream = [("xgmi", 2), ("xgmi", 4), ("xgmiw", 2), ("xgmiw", 4)]
@@ -436,6 +455,33 @@ class GpuBackend:
                 print("xGMI exchange failed its checksum verification; using RCCL",
                       file=sys.stderr)
                 self._set_mode(rest[0])
+
+    def _calibrate_keyed(self, iters):
+        """The key-cached xGMI exchange: the read-form Pull (psg_xgmi_pull_slots)
+        or the write form (psg_xgmi_pull_write_slots), whichever runs faster
+        here (max over ranks).  PSG_BENCH_EXCHANGE=xgmi-keyed / xgmi-keyed-w forces one."""
+        cands = ["xgmi-keyed", "xgmi-keyed-w"]
+        forced = os.environ.get("PSG_BENCH_EXCHANGE")
+        if forced:
+            cands = [c for c in cands if c == forced]
+            if not cands:
+                raise SystemExit(f"PSG_BENCH_EXCHANGE={forced}: not available here")
+        times = []
+        for c in cands:
+            self.mode = c
+            self._one_step()
+            self.sync()
+            self.group.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                self._one_step()
+            self.sync()
+            times.append((time.perf_counter() - t0) * 1e3 / iters)
+            self.group.barrier()
+        t = self.group.allreduce_max(times)
+        self.mode = cands[min(range(len(cands)), key=lambda i: t[i])]
+        self.calibration = {c: round(x, 4) for c, x in zip(cands, t)}
+        self.pushes_in_calibration = len(cands) * (iters + 1)
 
     def _verify_xgmi(self) -> bool:
         """One xGMI Push + Pull, then every rank's pulled block w must carry the
@@ -730,6 +776,9 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         elif getattr(backend, "mode", "") == "xgmi-keyed":
             res["config"]["exchange"] = ("keyed xGMI kernels on cached slots (psg_xgmi_push_slots / "
                                          "_pull_slots over the peers' values, stores and slot lists)")
+        elif getattr(backend, "mode", "") == "xgmi-keyed-w":
+            res["config"]["exchange"] = ("keyed xGMI kernels on cached slots, the Pull as writes "
+                                         "(psg_xgmi_push_slots / _pull_write_slots into every rank's output)")
         elif getattr(backend, "keyed", False):
             res["config"]["exchange"] = "RCCL grouped reduce / broadcast of the key-range segments"
         else:

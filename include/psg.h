@@ -348,6 +348,12 @@ int psg_xgmi_push_slots(psg_xgmi* x, psg_store* shard, const uint32_t* slots, ui
 int psg_xgmi_pull_slots(psg_xgmi* x, psg_store* shard, const uint32_t* const* peer_slots,
                         const uint64_t* seg_off_host, const uint64_t* seg_n_host, void* out,
                         psg_stream stream);
+/* The keyed Pull as writes (outputs registered with psg_xgmi_set_outs): rank r
+ * writes store[slots[i]] into out_w[seg_off + i] of every rank w.  Needs only
+ * this rank's own push_slots to be complete; one barrier per step, as for
+ * psg_xgmi_pull_write. */
+int psg_xgmi_pull_write_slots(psg_xgmi* x, psg_store* shard, const uint32_t* slots, uint64_t seg_off,
+                              uint64_t seg_n, psg_stream stream);
 /* Host barrier of the ranks of one node over a POSIX shared-memory page. */
 int psg_node_barrier_create(const char* name, int nranks, int rank, psg_barrier** out);
 int psg_node_barrier_wait(psg_barrier* b, double timeout_s);

@@ -173,6 +173,41 @@ __global__ __launch_bounds__(256) void k_xgmi_push_slots(typename Elem<DT>::T* _
   }
 }
 
+// The keyed Pull as writes: rank r reads its segment through its own slots
+// (local) and writes it into out_w[seg_off + i] of every rank w.  Four keys
+// per lane with 16-B slot loads, a 16-B store read when the four slots are
+// consecutive, and 16-B posted stores when the segment is 16-B aligned in the
+// outputs (vec); element stores otherwise.
+template <typename T>
+__global__ __launch_bounds__(256) void k_xgmi_scatter_slots(const T* __restrict__ store,
+                                                            const uint32_t* __restrict__ slots, Outs outs,
+                                                            int nout, uint64_t seg_off, uint64_t n, int vec) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t nq = vec ? n / 4 : 0;
+  if constexpr (sizeof(T) == 4) {
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nq; j += stride) {
+      const u32x4 sl = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(slots) + j);
+      const uint32_t p0 = sl[0];
+      u32x4 v;
+      if (sl[1] == p0 + 1 && sl[2] == p0 + 2 && sl[3] == p0 + 3 && (p0 & 3) == 0) {
+        v = *reinterpret_cast<const u32x4*>(store + p0);
+      } else {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(store);
+        v = u32x4{s32[sl[0]], s32[sl[1]], s32[sl[2]], s32[sl[3]]};
+      }
+#pragma unroll
+      for (int w = 0; w < kMaxPeers; ++w) {
+        if (w >= nout) break;
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(reinterpret_cast<T*>(outs.p[w]) + seg_off) + j);
+      }
+    }
+  }
+  for (uint64_t i = nq * 4 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const T v = store[slots[i]];
+    for (int w = 0; w < nout; ++w) reinterpret_cast<T*>(outs.p[w])[seg_off + i] = v;
+  }
+}
+
 struct SlotPeers {
   const uint32_t* slots[kMaxPeers];
   uint64_t off[kMaxPeers];
@@ -395,6 +430,41 @@ int psg_xgmi_pull_slots(psg_xgmi* x, psg_store* shard, const uint32_t* const* pe
     case 4: k_xgmi_pull_slots<uint32_t><<<grid, kBlock, 0, s>>>((uint32_t*)out, st, sp); break;
     case 8: k_xgmi_pull_slots<uint64_t><<<grid, kBlock, 0, s>>>((uint64_t*)out, st, sp); break;
     default: k_xgmi_pull_slots<uint16_t><<<grid, kBlock, 0, s>>>((uint16_t*)out, st, sp); break;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int psg_xgmi_pull_write_slots(psg_xgmi* x, psg_store* shard, const uint32_t* slots, uint64_t seg_off,
+                              uint64_t seg_n, psg_stream stream) {
+  PSG_REQUIRE(x && shard, PSG_ERR_INVALID, "psg_xgmi_pull_write_slots: null argument");
+  PSG_REQUIRE(x->outs[0] != nullptr, PSG_ERR_INVALID, "psg_xgmi_pull_write_slots: no outputs (psg_xgmi_set_outs)");
+  PSG_REQUIRE(shard->vals == x->stores[x->rank], PSG_ERR_INVALID,
+              "psg_xgmi_pull_write_slots: shard is not this rank's registered store");
+  if (seg_n == 0) return PSG_OK;
+  PSG_REQUIRE(slots, PSG_ERR_INVALID, "psg_xgmi_pull_write_slots: null slots");
+  const int es = shard->esize;
+  Outs o;
+  for (int w = 0; w < x->nranks; ++w) o.p[w] = (u32x4*)x->outs[w];
+  const int vec = (es == 4 && aligned16(slots) && aligned16(shard->vals) && (seg_off * es) % 16 == 0) ? 1 : 0;
+  const uint64_t units = vec ? seg_n / 4 : seg_n;
+  uint64_t g = (units + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 4;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  hipStream_t st = (hipStream_t)stream;
+  switch (es) {
+    case 4:
+      k_xgmi_scatter_slots<uint32_t><<<(unsigned)g, kBlock, 0, st>>>((const uint32_t*)shard->vals, slots, o,
+                                                                     x->nranks, seg_off, seg_n, vec);
+      break;
+    case 8:
+      k_xgmi_scatter_slots<uint64_t><<<(unsigned)g, kBlock, 0, st>>>((const uint64_t*)shard->vals, slots, o,
+                                                                     x->nranks, seg_off, seg_n, 0);
+      break;
+    default:
+      k_xgmi_scatter_slots<uint16_t><<<(unsigned)g, kBlock, 0, st>>>((const uint16_t*)shard->vals, slots, o,
+                                                                     x->nranks, seg_off, seg_n, 0);
   }
   PSG_HIP(hipGetLastError());
   return PSG_OK;

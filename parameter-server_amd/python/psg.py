@@ -51,6 +51,7 @@ EXPORTS = [
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
     "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_xgmi_push_range",
     "psg_xgmi_pull_range", "psg_xgmi_set_outs", "psg_xgmi_pull_write_range", "psg_xgmi_pull_write",
+    "psg_xgmi_pull_write_slots",
     "psg_xgmi_push_slots", "psg_xgmi_pull_slots", "psg_node_barrier_create",
     "psg_node_barrier_wait", "psg_node_barrier_destroy",
 ]
@@ -142,6 +143,7 @@ def lib() -> C.CDLL:
             "psg_xgmi_set_outs": ([vp, C.POINTER(vp)], i32),
             "psg_xgmi_pull_write_range": ([vp, vp, u64, u64, u64, vp], i32),
             "psg_xgmi_pull_write": ([vp, vp, u64, vp], i32),
+            "psg_xgmi_pull_write_slots": ([vp, vp, vp, u64, u64, vp], i32),
             "psg_xgmi_push_slots": ([vp, vp, vp, u64, u64, vp], i32),
             "psg_xgmi_pull_slots": ([vp, vp, C.POINTER(vp), vp, vp, vp, vp], i32),
             "psg_node_barrier_create": ([C.c_char_p, i32, i32, C.POINTER(vp)], i32),
@@ -522,6 +524,9 @@ class Xgmi:
 
     def pull_write_range(self, shard: Store, n_total: int, off: int, cnt: int, stream=None) -> None:
         _call("psg_xgmi_pull_write_range", self.h, shard.h, n_total, off, cnt, _s(stream))
+
+    def pull_write_slots(self, shard: Store, slots, seg_off: int, seg_n: int, stream=None) -> None:
+        _call("psg_xgmi_pull_write_slots", self.h, shard.h, _ptr(slots), seg_off, seg_n, _s(stream))
 
     def push_slots(self, shard: Store, slots, seg_off: int, seg_n: int, stream=None) -> None:
         _call("psg_xgmi_push_slots", self.h, shard.h, _ptr(slots), seg_off, seg_n, _s(stream))

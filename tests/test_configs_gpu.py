@@ -139,12 +139,17 @@ def test_xgmi_double_buffered_ragged_chunks():
     assert "double-buffered over 4 chunks" in res["config"]["exchange"]
 
 
-def test_configs3_keyed_cached_n4_xgmi_shared_gpu():
+@pytest.mark.parametrize("exchange", ["xgmi-keyed", "xgmi-keyed-w"])
+def test_configs3_keyed_cached_n4_xgmi_shared_gpu(exchange):
     """configs[3] across ranks: nw = ns = 4, 10 M sorted uint64 keys, LR key
     caching — each shard resolves its psg_slice segment once, then Push / Pull
-    run as the keyed xGMI kernels on the cached slots; every rank's whole pulled
-    vector is checked against the closed form of the pushes."""
-    res = _bench_shared(4, ["--workload", "keyed-cached", "--steps", "3", "--warmup", "1"], {})
+    run as the keyed xGMI kernels on the cached slots, the Pull as reads of the
+    owners' stores or as writes into every rank's output (forced each way);
+    every rank's whole pulled vector is checked against the closed form of the
+    pushes."""
+    res = _bench_shared(4, ["--workload", "keyed-cached", "--steps", "3", "--warmup", "1"],
+                        {"PSG_BENCH_EXCHANGE": exchange})
     assert res["parity_check"] is True, res
     assert res["config"]["keys_per_worker"] == 10_000_000 and res["n_gpus"] == 4
     assert "keyed xGMI" in res["config"]["exchange"], res["config"]
+    assert ("as writes" in res["config"]["exchange"]) == exchange.endswith("-w"), res["config"]
