@@ -797,8 +797,9 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
     elif world == 1 and getattr(backend, "keyed", False):
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
                                    "SORTED-store Push: k_validate_windows + k_resolve_apply "
-                                   "(whole-request validation before any write; one host sync; "
-                                   "one server, so no slicer pass)", vb)
+                                   "(whole-request validation before any write; tile windows "
+                                   "cached per key array; completion word written by the "
+                                   "kernel; one server, so no slicer pass)", vb)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
                                    "k_dense_vec<PUSH> (store += vals)", vb)

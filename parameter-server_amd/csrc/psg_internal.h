@@ -156,7 +156,29 @@ struct psg_store {
   // store-writing kernel of that request reads it first and writes nothing.
   int* reject_dev;
   int seq;           // request sequence number (never 0 after the first request)
-  uint32_t done_seq; // completion words the stream has been asked to write
+  uint32_t done_seq; // completion words the stream or a kernel has been asked to write
+  // k_resolve_apply signals its own completion: every block counts itself in
+  // on one of 8 shard counters, each shard's last block on a top counter, and
+  // the block that completes the top writes the completion word
+  // (psg_store.hip, block_arrive / request_done).  Counters are monotonic;
+  // ctr_base holds each one's value before the next launch.
+  uint32_t* done_ctr;
+  uint32_t ctr_base[9];
+  // K's generation: bumped whenever the sorted key array changes (insert,
+  // clear), so a cached window of an older K is never trusted.
+  uint32_t gen;
+  // Store-key windows per request tile, cached per request key array (the
+  // LR / benchmark steady state sends the same key list again and again).
+  struct WinCache {
+    const uint64_t* q;   // request keys (device pointer) the entry was filled for
+    uint64_t n;
+    void* win;           // device psg::Win[ntiles]
+    uint64_t cap_tiles;
+    uint64_t last_use;
+    int trusted;         // skip the search pre-pass; the kernel still verifies
+    int strikes;         // kernel-detected stale windows for this (q, n)
+  } wc[4];
+  uint64_t wc_clock;
 };
 
 struct psg_adam {

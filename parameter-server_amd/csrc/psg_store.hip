@@ -13,10 +13,18 @@
 //               strictly ascending and inside the shard's range, or the whole
 //               request is rejected before anything is written; and, per
 //               request tile, the window of K its first and last key bracket
-//               (one 64-ary search per tile end);
+//               (one 64-ary search per tile end) — skipped when the windows
+//               cached for this key array are trusted (below);
 //             k_resolve_apply     stages each tile's window of K into LDS,
 //               places every key by an LDS search / merge walk and applies the
-//               request to the found slots (store[slot] += val, out = store).
+//               request to the found slots (store[slot] += val, out = store),
+//               then signals the request's completion itself (block_arrive).
+//           A tile's window depends only on K and the tile's first and last
+//           key, so windows are cached per request key array (the LR and
+//           benchmark steady state repeats one key list): k_resolve_apply
+//           checks each cached window against its tile's end keys and, on a
+//           mismatch, searches it inline.  A Pull on trusted windows is ONE
+//           kernel; a Push is the key-stream validation plus that kernel.
 //           Keys that are absent are inserted with value 0 afterwards — the
 //           `operator[]` insert of KVApp.h:449/452 — by a parallel merge of the
 //           (compacted, sorted) new keys into K and V, and the request is
@@ -43,13 +51,71 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // (one plain store of 1 per wave that saw the condition — idempotent, no
 // atomics), so a request needs no flag reset launch and no flag copy: the
 // host zeroes them before the launch and reads them after the stream sync.
-enum { F_MISSING = 0, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
+// F_WINMISS: a cached window did not match its tile (searched inline).
+enum { F_MISSING = 0, F_WINMISS = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
 // the host-memory word after the flags that the stream's completion write
 // targets (read_flags); never zeroed by reset_flags
 constexpr int kDoneWord = F_NFLAGS;
 
 __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
   if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
+}
+
+// The store-key window of one request tile: [lo, hi) of K brackets every key
+// between the tile's first and last key (lo = lower_bound(K, first), hi =
+// lower_bound(K, last) + 1, clipped to S).  Valid while K is unchanged (gen).
+struct Win {
+  uint64_t first, last;
+  uint32_t lo, hi, gen, pad;
+};
+
+// Completion of a request, signalled by its last kernel (k_resolve_apply)
+// instead of a stream-written word, which costs a separate blit launch (~8.6
+// us per request on MI355X).  Each block, once it knows every host flag it
+// will raise (after the resolve of its last tile), raises them, makes them
+// visible at system scope (flag_fence), and counts itself in with a returning
+// atomic on one of 8 shard counters (blockIdx mod 8, each on its own lines,
+// so 2048 arrivals do not queue on one address); its apply stores go out
+// while that round trip is in flight.  The last block of a shard counts the
+// shard in on the top counter, and the block that completes the top writes
+// the host-mapped completion word.  Counters are monotonic: the host passes
+// the value each one's last add returns (Arrival).  Stores to the store and
+// the reply need no ordering here: only later launches on the same stream
+// read them.  (A posted per-block word in host memory instead — no atomic —
+// took 50-90 us to land for 2048 blocks: PCIe writes serialise.)
+constexpr int kArriveShards = 8;
+constexpr int kArriveStride = 64;  // words between counters (256 B)
+struct Arrival {
+  uint32_t* ctr;  // kArriveShards shard counters, then the top counter
+  uint32_t last[kArriveShards];
+  uint32_t top_last;
+};
+__device__ __forceinline__ void flag_fence(bool raised) {
+  if (__ballot(raised)) __threadfence_system();
+}
+__device__ __forceinline__ uint32_t block_arrive(int* flags, int missing, int winmiss, int range, int unsorted,
+                                                 const Arrival& a) {
+  raise_flag(flags, F_MISSING, missing != 0);
+  raise_flag(flags, F_WINMISS, winmiss != 0);
+  raise_flag(flags, F_RANGE, range != 0);
+  raise_flag(flags, F_UNSORTED, unsorted != 0);
+  flag_fence((missing | winmiss | range | unsorted) != 0);
+  __syncthreads();
+  uint32_t old = 0;
+  if (threadIdx.x == 0)
+    old = __hip_atomic_fetch_add(a.ctr + (blockIdx.x % kArriveShards) * kArriveStride, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+  return old;
+}
+__device__ __forceinline__ void request_done(uint32_t ticket, const Arrival& a, uint32_t* word, uint32_t val) {
+  if (threadIdx.x == 0 && ticket == a.last[blockIdx.x % kArriveShards]) {
+    const uint32_t top = __hip_atomic_fetch_add(a.ctr + kArriveShards * kArriveStride, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (top == a.top_last) {
+      __threadfence_system();
+      __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__ a, uint64_t lo,
@@ -199,13 +265,16 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 
 // Pass 1 of a SORTED request: validate the whole request and find each
 // tile's window of K, as two kinds of 256-thread blocks of one launch:
-//   blocks [0, nsearch)  one wave per window bound: wlo[t] = lower_bound(K,
-//                        q[t * tileN]) for t < ntiles, wlo[ntiles] =
-//                        lower_bound(K, q[n - 1]) + 1 (a 64-ary search, ~4
-//                        dependent scattered probes of 512 B);
+//   blocks [0, nsearch)  one wave per window bound: win[t].lo = lower_bound(K,
+//                        first key of tile t), win[t].hi = lower_bound(K, last
+//                        key of tile t) + 1 (a 64-ary search each, ~4
+//                        dependent scattered probes of 512 B), tagged with K's
+//                        generation and the two keys;
 //   the other blocks     stream the request keys (8 per lane, 16-B loads) and
 //                        check strict ascent — against the key before each
 //                        lane's eight — and the shard's range [kb, ke).
+// Either kind may be absent (nsearch = 0: the windows cached for this key
+// array are trusted; no stream blocks: a Pull, which checks its own keys).
 // The search blocks come first in dispatch order, so their latency runs under
 // the key stream.  An invalid request sets *reject = seq, which
 // k_resolve_apply checks before it writes anything, and raises F_UNSORTED /
@@ -214,20 +283,31 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 // Cache) plus the probes.
 __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __restrict__ q, uint64_t n,
                                                           const uint64_t* __restrict__ K, uint64_t S,
-                                                          uint64_t* __restrict__ wlo, uint64_t tileN,
+                                                          Win* __restrict__ win, uint32_t gen, uint64_t tileN,
                                                           unsigned nsearch, uint64_t kb, uint64_t ke,
                                                           int* __restrict__ reject, int seq,
                                                           int* __restrict__ flags, int vec) {
   const uint64_t ntiles = (n + tileN - 1) / tileN;
   if (blockIdx.x < nsearch) {
     const uint64_t waves = (uint64_t)nsearch * (kBlock / 64);
-    for (uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t <= ntiles; t += waves) {
-      if (t < ntiles) {
-        const uint64_t r = lower_bound_wave(K, S, q[t * tileN]);
-        if ((threadIdx.x & 63) == 0) wlo[t] = r;
+    for (uint64_t b = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); b < 2 * ntiles; b += waves) {
+      const uint64_t t = b >> 1;
+      const uint64_t t1 = (t + 1) * tileN < n ? (t + 1) * tileN : n;
+      if ((b & 1) == 0) {
+        const uint64_t key = q[t * tileN];
+        const uint64_t r = lower_bound_wave(K, S, key);
+        if ((threadIdx.x & 63) == 0) {
+          win[t].first = key;
+          win[t].lo = (uint32_t)r;
+          win[t].gen = gen;
+        }
       } else {
-        const uint64_t h = lower_bound_wave(K, S, q[n - 1]);
-        if ((threadIdx.x & 63) == 0) wlo[t] = h < S ? h + 1 : S;
+        const uint64_t key = q[t1 - 1];
+        const uint64_t h = lower_bound_wave(K, S, key);
+        if ((threadIdx.x & 63) == 0) {
+          win[t].last = key;
+          win[t].hi = (uint32_t)(h < S ? h + 1 : S);
+        }
       }
     }
     return;
@@ -301,41 +381,71 @@ __global__ __launch_bounds__(256) void k_validate_keys(const uint64_t* __restric
 // instead of 36: request key 8 + store key 8 + value 4 + store value 8).  An
 // absent key is skipped (a pull reads 0, what its insertion gives); the flags
 // tell the host to insert it and apply the request to it afterwards.
+template <int NT>
+__device__ __forceinline__ void stage_window(uint64_t* sK, const uint64_t* __restrict__ K, uint64_t lo,
+                                             uint64_t W) {
+  // straight to LDS (no VGPRs): each wave instruction moves 1 KiB of the
+  // window; lanes past its end re-read its start (written, never read).  A
+  // lane may read 8 B past K[S-1]: the key arrays carry kKeyPad spare elements
+  // for it.
+  const uint32_t nbytes = (uint32_t)W * 8u;
+  const char* src = reinterpret_cast<const char*>(K + lo);
+  for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += (NT / 64) * 1024u) {
+    const uint32_t off = c + (threadIdx.x & 63) * 16u;
+    const char* g = off < nbytes ? src + off : src;
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)((char*)sK + c), 16, 0, 0);
+  }
+}
+
+// __launch_bounds__(NT, 8): 8 waves per SIMD, i.e. two 1024-thread blocks per
+// CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
+// instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
+// and the 10 M-key Pull took 56 us instead of 40.
 template <int DT, int OP, int NT>
-__global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
+__global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
                                                        const uint64_t* __restrict__ K, uint64_t S,
-                                                       const uint64_t* __restrict__ wlo, uint64_t kb,
+                                                       Win* __restrict__ win, uint32_t gen, uint64_t kb,
                                                        uint64_t ke,
                                                        typename Elem<DT>::T* __restrict__ V,
                                                        const typename Elem<DT>::T* __restrict__ vals,
                                                        typename Elem<DT>::T* __restrict__ outv,
                                                        const int* __restrict__ reject, int seq,
-                                                       int* __restrict__ flags, int vec) {
+                                                       int* __restrict__ flags, int vec,
+                                                       Arrival arrival, uint32_t* __restrict__ done_word,
+                                                       uint32_t done_val) {
   using E = Elem<DT>;
   using T = typename E::T;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
   constexpr uint32_t winN = 2 * NT * kPerLane;          // LDS window of store keys
   __shared__ uint64_t sK[winN];
+  __shared__ uint64_t sBound[2];
   // A request that writes the store was validated as a whole first: if
-  // k_validate_windows rejected it, write nothing (a uniform early exit of
-  // every block before any store access).  A Pull writes only its reply, so
-  // it checks its keys here, in the same pass (CHECK), and the host rejects it
-  // from the flags before anything else happens (no insert of absent keys).
+  // k_validate_windows rejected it, write nothing (every block skips its
+  // tiles, uniformly, before any store access, and still signals).  A Pull
+  // writes only its reply, so it checks its keys here, in the same pass
+  // (CHECK), and the host rejects it from the flags before anything else
+  // happens (no insert of absent keys).
   constexpr bool CHECK = OP == PSG_PULL;
-  if constexpr (!CHECK) {
-    if (*reject == seq) return;
-  }
-  int missing = 0, range = 0, unsorted = 0;
-  const uint64_t ntiles = (n + tileN - 1) / tileN;
+  bool skip = false;
+  if constexpr (!CHECK) skip = *reject == seq;
+  int missing = 0, range = 0, unsorted = 0, winmiss = 0;
+  uint32_t ticket = 0;
+  bool arrived = false;
+  const uint64_t ntiles = skip ? 0 : (n + tileN - 1) / tileN;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * tileN;
     const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
-    const uint64_t lo = wlo[tile];
-    uint64_t hi = tile + 1 < ntiles ? wlo[tile + 1] + 1 : wlo[ntiles];
+    // the window cached for this tile, staged speculatively: it is right when
+    // it was computed against this K for this tile's first and last key
+    // (checked below, once those keys have arrived with the rest)
+    const Win e = win[tile];
+    const bool cur = e.gen == gen;
+    uint64_t lo = cur ? e.lo : 0, hi = cur ? e.hi : 0;
     if (hi > S) hi = S;
     if (hi < lo) hi = lo;  // unsorted input
-    const uint64_t W = hi - lo;
-    const bool staged = W <= (uint64_t)winN;
+    uint64_t W = hi - lo;
+    bool staged = W <= (uint64_t)winN;
     const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
     const bool whole = i0 + kPerLane <= t1;
     // Issue every global load that does not depend on the window before the
@@ -343,20 +453,8 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
     // before them and (Push) its values — so a tile costs two dependent HBM
     // round trips (these, then the store values) instead of one per staging
     // step plus two.
-    if (staged) {
-      // straight to LDS (no VGPRs): each wave instruction moves 1 KiB of the
-      // window; lanes past its end re-read its start (written, never read).
-      // A lane may read 8 B past K[S-1]: the key arrays carry kKeyPad spare
-      // elements for it.
-      const uint32_t nbytes = (uint32_t)W * 8u;
-      const char* src = reinterpret_cast<const char*>(K + lo);
-      for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nbytes; c += (NT / 64) * 1024u) {
-        const uint32_t off = c + (threadIdx.x & 63) * 16u;
-        const char* g = off < nbytes ? src + off : src;
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)((char*)sK + c), 16, 0, 0);
-      }
-    }
+    if (cur && staged) stage_window<NT>(sK, K, lo, W);
+    const uint64_t qfirst = q[t0], qlast = q[t1 - 1];
     uint64_t key[kPerLane];
     if (whole && (vec & 2)) {
       const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0);
@@ -412,6 +510,32 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
     // of the window before it has landed.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (!(cur && e.first == qfirst && e.last == qlast)) {
+      // stale or absent window (block-uniform): search both ends (waves 0 and
+      // 1), keep the result for the next request on these keys, restage
+      const int wv = threadIdx.x >> 6;
+      if (wv < 2) {
+        const uint64_t r = lower_bound_wave(K, S, wv == 0 ? qfirst : qlast);
+        if ((threadIdx.x & 63) == 0) sBound[wv] = r;
+      }
+      __syncthreads();
+      lo = sBound[0];
+      hi = sBound[1] < S ? sBound[1] + 1 : S;
+      if (hi < lo) hi = lo;
+      W = hi - lo;
+      staged = W <= (uint64_t)winN;
+      if (threadIdx.x == 0) {
+        win[tile].first = qfirst;
+        win[tile].last = qlast;
+        win[tile].lo = (uint32_t)lo;
+        win[tile].hi = (uint32_t)hi;
+        win[tile].gen = gen;
+      }
+      if (staged) stage_window<NT>(sK, K, lo, W);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      winmiss = 1;
+    }
     uint32_t r = 0;
     uint64_t slot[kPerLane];
     bool hit[kPerLane];
@@ -441,6 +565,10 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
       hit[k] = found;
       slot[k] = p;
       if (!found) missing++;
+    }
+    if (tile + gridDim.x >= ntiles) {  // this block's last tile (uniform)
+      ticket = block_arrive(flags, missing, winmiss, range, unsorted, arrival);
+      arrived = true;
     }
     // apply.  A lane whose 4 keys are 4 consecutive, 16-B aligned store
     // slots (the common case: a request that covers a stretch of the store)
@@ -494,11 +622,8 @@ __global__ __launch_bounds__(NT) void k_resolve_apply(const uint64_t* __restrict
     }
     __syncthreads();
   }
-  raise_flag(flags, F_MISSING, missing != 0);
-  if constexpr (CHECK) {
-    raise_flag(flags, F_RANGE, range != 0);
-    raise_flag(flags, F_UNSORTED, unsorted != 0);
-  }
+  if (!arrived) ticket = block_arrive(flags, missing, winmiss, range, unsorted, arrival);  // no tile (rejected)
+  request_done(ticket, arrival, done_word, done_val);
 }
 
 // Block-wide exclusive scan helper over 256 lanes (wave = 64).
@@ -806,6 +931,7 @@ static int merge_insert(psg_store* s, const uint64_t* miss, uint64_t m, hipStrea
   s->vals = V2;
   s->size = S + m;
   s->capacity = cap;
+  s->gen++;  // every cached window belongs to the old K
   return PSG_OK;
 }
 
@@ -859,27 +985,71 @@ static int ra_block() {
   return nt;
 }
 
+// The window cache entry for request keys (q, n): the entry last filled for
+// them, else the least recently used one (its windows stay correct for any
+// tile whose end keys they match, so it needs no clearing).
+static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t n, uint64_t ntiles) {
+  psg_store::WinCache* e = nullptr;
+  for (auto& c : s->wc)
+    if (c.win && c.q == q && c.n == n) e = &c;
+  if (!e) {
+    e = &s->wc[0];
+    for (auto& c : s->wc)
+      if (c.last_use < e->last_use) e = &c;
+    e->q = q;
+    e->n = n;
+    e->trusted = 0;
+    e->strikes = 0;
+  }
+  if (e->cap_tiles < ntiles) {
+    if (e->win) (void)hipFree(e->win);
+    e->win = nullptr;
+    e->cap_tiles = 0;
+    const uint64_t cap = std::max<uint64_t>(ntiles, 64);
+    if (hipMalloc(&e->win, cap * sizeof(Win)) != hipSuccess) return nullptr;
+    // gen 0 never matches a store generation: a fresh entry is all misses
+    if (hipMemset(e->win, 0, cap * sizeof(Win)) != hipSuccess) return nullptr;
+    e->cap_tiles = cap;
+    e->trusted = 0;
+  }
+  e->last_use = ++s->wc_clock;
+  return e;
+}
+
 template <int DT, int OP>
-static void launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals,
-                                 void* out, hipStream_t st) {
+static int launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals,
+                                void* out, Win* win, uint32_t done_val, hipStream_t st) {
   using T = typename Elem<DT>::T;
   const int nt = ra_block();
   const uint64_t ntiles = (n + (uint64_t)nt * kPerLane - 1) / ((uint64_t)nt * kPerLane);
   // bit 0: request values / replies 16-B aligned; bit 1: request keys 16-B aligned
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
                   (aligned16(q) ? 2 : 0);
+  const unsigned g = grid_n(ntiles, 1);
+  Arrival arr;
+  arr.ctr = s->done_ctr;
+  unsigned nsh = 0;
+  for (int j = 0; j < kArriveShards; ++j) {
+    const uint32_t cnt = g > (unsigned)j ? (g - 1 - j) / kArriveShards + 1 : 0;
+    arr.last[j] = s->ctr_base[j] + cnt - 1;  // unused when cnt == 0
+    nsh += cnt ? 1 : 0;
+  }
+  arr.top_last = s->ctr_base[kArriveShards] + nsh - 1;
+#define PSG_RA_ARGS                                                                                     \
+  q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end, (T*)s->vals, (const T*)vals, (T*)out, \
+      s->reject_dev, s->seq, s->flags, vec, arr, reinterpret_cast<uint32_t*>(s->flags + kDoneWord), done_val
   if (nt == 1024)
-    k_resolve_apply<DT, OP, 1024><<<grid_n(ntiles, 1), 1024, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
-                                                                     s->key_end, (T*)s->vals, (const T*)vals,
-                                                                     (T*)out, s->reject_dev, s->seq, s->flags, vec);
+    k_resolve_apply<DT, OP, 1024><<<g, 1024, 0, st>>>(PSG_RA_ARGS);
   else if (nt == 512)
-    k_resolve_apply<DT, OP, 512><<<grid_n(ntiles, 1), 512, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
-                                                                   s->key_end, (T*)s->vals, (const T*)vals,
-                                                                   (T*)out, s->reject_dev, s->seq, s->flags, vec);
+    k_resolve_apply<DT, OP, 512><<<g, 512, 0, st>>>(PSG_RA_ARGS);
   else
-    k_resolve_apply<DT, OP, 256><<<grid_n(ntiles, 1), 256, 0, st>>>(q, n, s->keys, s->size, s->wlo, s->key_begin,
-                                                                   s->key_end, (T*)s->vals, (const T*)vals,
-                                                                   (T*)out, s->reject_dev, s->seq, s->flags, vec);
+    k_resolve_apply<DT, OP, 256><<<g, 256, 0, st>>>(PSG_RA_ARGS);
+#undef PSG_RA_ARGS
+  PSG_HIP(hipGetLastError());
+  // every block counted itself in on its shard, every non-empty shard on the top
+  for (int j = 0; j < kArriveShards; ++j) s->ctr_base[j] += g > (unsigned)j ? (g - 1 - j) / kArriveShards + 1 : 0;
+  s->ctr_base[kArriveShards] += nsh;
+  return PSG_OK;
 }
 
 // A new request: its sequence number tags the reject word (never reset: a
@@ -889,28 +1059,70 @@ static int next_seq(psg_store* s) {
   return s->seq;
 }
 
+// Wait for the completion word k_resolve_apply writes (request_done); after
+// 2 ms (a long request, or a fault) fall back to hipStreamSynchronize, which
+// also reports any error.  PSG_SYNC_POLL=0 always synchronises the stream.
+static int wait_done(psg_store* s, uint32_t want, hipStream_t st) {
+  if (sync_poll()) {
+    const volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(s->flags_host + kDoneWord);
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      if (*w == want) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return PSG_OK;
+      }
+      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  PSG_HIP(hipStreamSynchronize(st));
+  return PSG_OK;
+}
+
+// Window-cache policy.  A key array seen before whose windows the previous
+// request confirmed skips the search pre-pass (trusted); the kernel still
+// checks every window and searches a stale one inline (F_WINMISS).  A key
+// array that keeps changing under one pointer (two misses) always gets the
+// pre-pass, so it never pays the slower inline searches twice.
 template <int DT>
 static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals,
                          void* out, hipStream_t st) {
   const int nt = ra_block();
   const uint64_t tile = (uint64_t)nt * kPerLane;
   const uint64_t ntiles = (n + tile - 1) / tile;
+  psg_store::WinCache* wc = win_entry(s, q, n, ntiles);
+  PSG_REQUIRE(wc, PSG_ERR_HIP, "SORTED store: window cache allocation failed");
+  Win* win = static_cast<Win*>(wc->win);
+  static const int cache_on = [] {
+    const char* e = getenv("PSG_WIN_CACHE");  // 0: always run the search pre-pass (A/B)
+    return e ? atoi(e) : 1;
+  }();
+  const bool trusted = cache_on && wc->trusted != 0 && (uint32_t)wc->trusted == s->gen;
   reset_flags(s);
   const int seq = next_seq(s);
-  // search blocks: one wave per window bound (ntiles + 1 of them); key-stream
-  // blocks: 1024 keys each, capped at the streaming grid
-  const unsigned nsearch = (unsigned)((ntiles + 1 + kBlock / 64 - 1) / (kBlock / 64));
-  // a Pull checks its keys inside k_resolve_apply: window searches only
+  // search blocks: one wave per window bound (2 per tile); key-stream blocks:
+  // 2048 keys each, capped at the streaming grid.  A Pull checks its keys
+  // inside k_resolve_apply, so on trusted windows it is one launch.
+  const unsigned nsearch = trusted ? 0u : (unsigned)((2 * ntiles + kBlock / 64 - 1) / (kBlock / 64));
   const unsigned nval = op == PSG_PULL ? 0u : grid_n(n, (uint64_t)kBlock * 8);
-  k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, s->wlo, tile, nsearch,
-                                                       s->key_begin, s->key_end, s->reject_dev, seq, s->flags,
-                                                       aligned16(q) ? 1 : 0);
-  switch (op) {
-    case PSG_PUSH: launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, st); break;
-    case PSG_PULL: launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, st); break;
-    default: launch_resolve_apply<DT, PSG_PUSH | PSG_PULL>(s, q, n, vals, out, st); break;
-  }
+  if (nsearch + nval > 0)
+    k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
+                                                         s->key_begin, s->key_end, s->reject_dev, seq, s->flags,
+                                                         aligned16(q) ? 1 : 0);
   PSG_HIP(hipGetLastError());
+  const uint32_t want = ++s->done_seq;
+  switch (op) {
+    case PSG_PUSH: PSG_TRY((launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, win, want, st))); break;
+    case PSG_PULL: PSG_TRY((launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, win, want, st))); break;
+    default: PSG_TRY((launch_resolve_apply<DT, PSG_PUSH | PSG_PULL>(s, q, n, vals, out, win, want, st))); break;
+  }
+  PSG_TRY(wait_done(s, want, st));
+  if (s->flags_host[F_WINMISS]) {
+    wc->trusted = 0;
+    wc->strikes++;
+  } else if (wc->strikes < 2 && !s->flags_host[F_UNSORTED] && !s->flags_host[F_RANGE]) {
+    wc->trusted = (int)s->gen;  // trusted while K keeps this generation
+  }
   return PSG_OK;
 }
 
@@ -940,8 +1152,9 @@ static int sorted_request(psg_store* s, int op, const uint64_t* q, const void* v
     PSG_TRY(read_flags(s, st));
     PSG_TRY(check_request_flags(s));
     PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
+    PSG_TRY(read_flags(s, st));
   }
-  PSG_TRY(read_flags(s, st));
+  // (the fused form has waited for its own completion word)
   PSG_TRY(check_request_flags(s));  // rejected by k_validate_windows: nothing was written
   if (s->flags_host[F_MISSING] == 0) return PSG_OK;
   if (sorted_fused() && s->size > 0) {
@@ -1042,6 +1255,11 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
   if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
       (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(reject word)", __FILE__, __LINE__));
+  constexpr size_t kCtrBytes = (kArriveShards + 1) * kArriveStride * sizeof(uint32_t);
+  if ((e = hipMalloc((void**)&s->done_ctr, kCtrBytes)) != hipSuccess ||
+      (e = hipMemset(s->done_ctr, 0, kCtrBytes)) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(completion counters)", __FILE__, __LINE__));
+  s->gen = 1;  // cached windows carry gen >= 1; zeroed entries never match
   if (kind == PSG_STORE_DENSE) {
     s->capacity = capacity;
     s->size = capacity;
@@ -1075,6 +1293,9 @@ int psg_store_destroy(psg_store* s) {
   if (s->wlo) (void)hipFree(s->wlo);
   if (s->flags_host) (void)hipHostFree(s->flags_host);
   if (s->reject_dev) (void)hipFree(s->reject_dev);
+  if (s->done_ctr) (void)hipFree(s->done_ctr);
+  for (auto& c : s->wc)
+    if (c.win) (void)hipFree(c.win);
   delete s;
   return PSG_OK;
 }
@@ -1098,6 +1319,7 @@ int psg_store_clear(psg_store* s, psg_stream stream) {
     PSG_HIP(hipMemsetAsync(s->vals, 0, s->capacity * s->esize, (hipStream_t)stream));
   } else {
     s->size = 0;
+    s->gen++;
   }
   return PSG_OK;
 }

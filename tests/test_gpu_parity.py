@@ -273,6 +273,62 @@ def test_sorted_rejected_request_leaves_a_populated_store_unchanged(bad, flags):
     np.testing.assert_array_equal(st.dump()[1], (v0 + np.float32(1)).astype(np.float32))
 
 
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64])
+def test_sorted_window_cache_transitions(dtype):
+    """The store-key windows are cached per request key array and trusted once
+    a request confirmed them; k_resolve_apply re-checks every cached window
+    against its tile's first and last key and searches a stale one inline.
+    One key buffer is reused with changing contents through every transition
+    — repeats (trusted, no pre-pass), new keys under the same pointer (stale
+    windows), inner keys changed with the ends kept, absent keys (an insert
+    changes K's generation), keys alternating under one pointer, a rejected
+    Pull on trusted windows — each request checked against the oracle."""
+    rng = np.random.default_rng(123)
+    univ = np.unique(rng.integers(1 << 20, 1 << 62, 400000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, dtype, 0, KMAX, 0)
+    orc = oracle.Store(dtype)
+    v0 = synth(len(univ), dtype, 5, 1, -1.0, 1.0)
+    st.handle(psg.PUSH, dev(univ), dev(v0), None, len(univ))
+    orc.handle(oracle.PUSH, univ, v0, len(univ))
+    n = 150000
+    a = np.sort(rng.choice(univ, n, replace=False))
+    b = np.sort(rng.choice(univ, n, replace=False))
+    inner = a.copy()
+    inner[1:-1] = np.sort(rng.choice(univ[(univ > a[0]) & (univ < a[-1])], n - 2, replace=False))
+    fresh = np.unique(np.concatenate([a[: n // 2], rng.integers(1 << 20, 1 << 62, n, dtype=np.uint64)]))[:n]
+    dk = psg.DeviceBuffer(n * 8)
+    dv = psg.DeviceBuffer(n * ES[dtype])
+    out = psg.DeviceBuffer(n * ES[dtype])
+    seq = [a, a, a, b, b, b, inner, inner, a, fresh, fresh, a, b, a, b, a, a]
+    for j, k in enumerate(seq):
+        flags = [psg.PUSH | psg.PULL, psg.PULL, psg.PUSH][j % 3]
+        v = synth(n, dtype, 900 + j, 1, -1.0, 1.0)
+        dk.upload(k)
+        dv.upload(v)
+        st.handle(flags, dk, dv if flags & psg.PUSH else None, out if flags & psg.PULL else None, n)
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
+        if flags & psg.PULL:
+            np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"request {j}")
+    # a Pull with one unsorted pair on trusted windows is rejected, store unchanged
+    dk.upload(a)
+    st.handle(psg.PULL, dk, None, out, n)
+    st.handle(psg.PULL, dk, None, out, n)
+    bad = a.copy()
+    bad[n // 2], bad[n // 2 + 1] = bad[n // 2 + 1], bad[n // 2]
+    dk.upload(bad)
+    k0, s0 = st.dump()
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PULL, dk, None, out, n)
+    assert ei.value.code == 1
+    k1, s1 = st.dump()
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_array_equal(s1, s0)
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv.view(NPT[dtype]), ov)
+
+
 def test_dense_keyed_rejected_request_leaves_the_store_unchanged():
     st = psg.Store(psg.DENSE, psg.F32, 100, 100000, 5000)
     base = np.arange(5000, dtype=np.float32)

@@ -10,6 +10,8 @@
 #   f16      1 G f16 bench line (configs[4])   e2e    C++ API end to end, 10 M keys
 #   t:EXPR   pytest -m gpu -k EXPR             pmck / pmckc  PMC traffic of the keyed /
 #                                                      key-cached Push (two passes each)
+#   trace    kernel trace of the keyed bench: durations and the idle gaps between
+#            launches (tools/trace_gaps.py)
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -41,6 +43,9 @@ for st in "$@"; do
           step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
           step 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_w_$st.log 2>&1; echo "$st write rc=$?"
           python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" 10000000 gpurun_out/$out $per ;;
+    trace) rm -rf gpurun_out/trace_keyed
+          step 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_keyed -o run -- python3 bench.py --workload keyed --no-cpu-baseline --no-probe256 --steps 10 --warmup 2 > gpurun_out/trace_keyed.json 2>&1; echo "trace rc=$?"
+          python3 tools/trace_gaps.py gpurun_out/trace_keyed/run_kernel_trace.csv 8 ;;
     f16) step 300 python3 bench.py --workload dense-f16 --no-cpu-baseline > gpurun_out/bench_f16.json 2> gpurun_out/bench_f16.err; echo "f16 rc=$?"; cat gpurun_out/bench_f16.json ;;
     e2e) step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 10000000 20 > gpurun_out/e2e_threads_10M.log 2>&1; echo "e2e threads rc=$?"; head -3 gpurun_out/e2e_threads_10M.log
          step 300 tests/_bin/kv_cluster_device -ns 1 -nw 1 -procs 10000000 20 > gpurun_out/e2e_procs_10M.log 2>&1; echo "e2e procs rc=$?"; head -3 gpurun_out/e2e_procs_10M.log
