@@ -176,7 +176,12 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * A DENSE store accepts only keys inside [key_begin, key_begin + capacity).
  * A request that breaks either rule fails (PSG_ERR_INVALID / PSG_ERR_RANGE)
  * and leaves the store unchanged; the contents of out are then unspecified.
- * vals/out are device arrays of n elements of the store's dtype. */
+ * vals/out are device arrays of n elements of the store's dtype.
+ * A keyed request on a SORTED store returns once its result is known (it
+ * waits for a completion word its own kernel writes); later work on `stream`
+ * is ordered after it.  The store remembers the LDS windows of the last few
+ * key arrays it saw (by device pointer and n) and verifies them per tile, so
+ * a caller may rewrite a key array in place between requests. */
 int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,
                      uint64_t first_key, const void* vals, void* out, uint64_t n,
                      psg_stream stream);
