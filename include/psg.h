@@ -177,9 +177,12 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * A request that breaks either rule fails (PSG_ERR_INVALID / PSG_ERR_RANGE)
  * and leaves the store unchanged; the contents of out are then unspecified.
  * vals/out are device arrays of n elements of the store's dtype.
- * A keyed request on a SORTED store returns once its result is known (it
- * waits for a completion word its own kernel writes); later work on `stream`
- * is ordered after it.  The store remembers the LDS windows of the last few
+ * A keyed request (SORTED store, or DENSE with keys) returns once the request
+ * has been checked and its keys and vals are no longer read — the caller may
+ * reuse them — while its last store and reply writes may still be in flight:
+ * work that reads out or the store must be ordered after it on `stream`.  (On
+ * the steady SORTED path it waits for a completion word its own kernel
+ * writes, not for the stream.)  The store remembers the LDS windows of the last few
  * key arrays it saw (by device pointer and n) and verifies them per tile, so
  * a caller may rewrite a key array in place between requests. */
 int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,

@@ -398,7 +398,10 @@ struct KVServerDefaultHandle {
       if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
       device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
                     "psg_store_handle");
-      device::Check(psg_stream_sync(s), "psg_stream_sync");
+      // psg_store_handle returns once the request's keys and vals are no longer
+      // read (psg.h), so a Push can be answered now; a Pull's reply must land
+      // first.  Later requests on this thread's stream are ordered behind it.
+      if (req_meta.pull) device::Check(psg_stream_sync(s), "psg_stream_sync");
       if (state->key_cache) Remember(dkeys, on_dev ? 0 : detail::KeyListHash(req_data.keys.data(), n), s);
     } else if (req_meta.push) {
       CHECK_EQ(n, req_data.vals.size());
