@@ -44,6 +44,7 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <random>
 #include <set>
 #include <thread>
 #include <unordered_map>
@@ -1093,21 +1094,53 @@ int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** a
   return rc;
 }
 
+// A port for the scheduler that no node of the job can be handed: every
+// server and worker listens on a kernel-chosen ephemeral port, so a port
+// taken from the ephemeral range (bind to 0, then close) could go to one of
+// them before the scheduler binds it — the job then fails with "ADD_NODE
+// request at a non-scheduler" or "Address already in use" (seen about once in
+// 20 launches with six jobs at a time).  So pick a free port BELOW the
+// ephemeral range (/proc/sys/net/ipv4/ip_local_port_range); only a process
+// that binds that very port explicitly could still collide.
+static int SchedulerPort() {
+  int eph_lo = 32768;
+  if (FILE* f = std::fopen("/proc/sys/net/ipv4/ip_local_port_range", "r")) {
+    int lo = 0, hi = 0;
+    if (std::fscanf(f, "%d %d", &lo, &hi) == 2 && lo > 0) eph_lo = lo;
+    std::fclose(f);
+  }
+  auto bindable = [](int port) {
+    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) return false;
+    sockaddr_in sa;
+    Resolve("127.0.0.1", port, &sa);
+    const bool ok = ::bind(fd, (sockaddr*)&sa, sizeof(sa)) == 0;
+    ::close(fd);
+    return ok;
+  };
+  const int base = 10000;
+  if (eph_lo - base >= 1000) {
+    std::mt19937 rng((uint32_t)getpid() ^ (uint32_t)std::chrono::steady_clock::now().time_since_epoch().count());
+    for (int tries = 0; tries < 200; ++tries) {
+      const int p = base + (int)(rng() % (uint32_t)(eph_lo - base));
+      if (bindable(p)) return p;
+    }
+  }
+  // no room below the ephemeral range: a kernel-chosen port (the old race)
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in sa;
+  Resolve("127.0.0.1", 0, &sa);
+  CHECK_EQ(::bind(fd, (sockaddr*)&sa, sizeof(sa)), 0);
+  socklen_t len = sizeof(sa);
+  getsockname(fd, (sockaddr*)&sa, &len);
+  ::close(fd);
+  return ntohs(sa.sin_port);
+}
+
 int Launch(int num_servers, int num_workers, int argc, char** argv) {
   CHECK_GT(num_servers, 0);
   CHECK_GT(num_workers, 0);
-  // a free port for the scheduler
-  int port = 0;
-  {
-    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    sockaddr_in sa;
-    Resolve("127.0.0.1", 0, &sa);
-    CHECK_EQ(::bind(fd, (sockaddr*)&sa, sizeof(sa)), 0);
-    socklen_t len = sizeof(sa);
-    getsockname(fd, (sockaddr*)&sa, &len);
-    port = ntohs(sa.sin_port);
-    ::close(fd);
-  }
+  const int port = SchedulerPort();
   const char* tmp = std::getenv("TMPDIR");
   std::string dir = std::string(tmp && *tmp ? tmp : "/tmp") + "/ps_procs_XXXXXX";
   std::vector<char> dbuf(dir.begin(), dir.end());
