@@ -369,15 +369,18 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("block", [256, 512, 1024])
-def test_sorted_store_every_block_size(block):
+@pytest.mark.parametrize("block,knobs", [(256, {}), (512, {}), (1024, {}),
+                                         (1024, {"PSG_WIN_CACHE": "0"}), (1024, {"PSG_SYNC_POLL": "0"})])
+def test_sorted_store_every_block_size(block, knobs):
     """PSG_RA_BLOCK is read once per process: each block size of the fused
-    validate / resolve / apply kernels gets a fresh process, every dtype."""
+    validate / resolve / apply kernels gets a fresh process, every dtype.  So
+    do the A/B switches: windows searched on every request (no window cache)
+    and the stream synchronised instead of the kernel's completion word."""
     import subprocess
     import sys
     paths = [os.path.join(os.path.dirname(HERE), "parameter-server_amd", "python"),
              os.path.join(os.path.dirname(HERE), "oracle")]
-    env = dict(os.environ, PSG_RA_BLOCK=str(block))
+    env = dict(os.environ, PSG_RA_BLOCK=str(block), **knobs)
     r = subprocess.run([sys.executable, "-c", _RA_BLOCK_CHILD.format(paths=paths)], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
