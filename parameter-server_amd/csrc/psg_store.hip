@@ -111,10 +111,11 @@ __device__ __forceinline__ void request_done(uint32_t ticket, const Arrival& a, 
   if (threadIdx.x == 0 && ticket == a.last[blockIdx.x % kArriveShards]) {
     const uint32_t top = __hip_atomic_fetch_add(a.ctr + kArriveShards * kArriveStride, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if (top == a.top_last) {
-      __threadfence_system();
-      __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    // no fence before the word: every block's flags were made visible before
+    // its arrival was counted (flag_fence), and the host reads nothing else
+    // (a system-scope fence here wrote back the XCD's L2 — every dirty store
+    // line of the apply — before the host could learn of the completion)
+    if (top == a.top_last) __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
