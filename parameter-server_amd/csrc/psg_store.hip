@@ -73,7 +73,7 @@ struct Win {
 // instead of a stream-written word, which costs a separate blit launch (~8.6
 // us per request on MI355X).  Each block, once it knows every host flag it
 // will raise (after the resolve of its last tile), raises them, makes them
-// visible at system scope (flag_fence), and counts itself in with a returning
+// visible at system scope (raise_flag_sys), and counts itself in with a returning
 // atomic on one of 8 shard counters (blockIdx mod 8, each on its own lines,
 // so 2048 arrivals do not queue on one address); its apply stores go out
 // while that round trip is in flight.  The last block of a shard counts the
@@ -90,16 +90,20 @@ struct Arrival {
   uint32_t last[kArriveShards];
   uint32_t top_last;
 };
-__device__ __forceinline__ void flag_fence(bool raised) {
-  if (__ballot(raised)) __threadfence_system();
+// A flag raised on the way to an arrival: a system-scope (write-through)
+// store, drained (vmcnt) before the block's barrier and so before its
+// arrival is counted — no fence, which would write back the XCD's L2.
+__device__ __forceinline__ void raise_flag_sys(int* flags, int which, bool cond) {
+  if (__ballot(cond) && (threadIdx.x & 63) == 0)
+    __hip_atomic_store(flags + which, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint32_t block_arrive(int* flags, int missing, int winmiss, int range, int unsorted,
                                                  const Arrival& a) {
-  raise_flag(flags, F_MISSING, missing != 0);
-  raise_flag(flags, F_WINMISS, winmiss != 0);
-  raise_flag(flags, F_RANGE, range != 0);
-  raise_flag(flags, F_UNSORTED, unsorted != 0);
-  flag_fence((missing | winmiss | range | unsorted) != 0);
+  raise_flag_sys(flags, F_MISSING, missing != 0);
+  raise_flag_sys(flags, F_WINMISS, winmiss != 0);
+  raise_flag_sys(flags, F_RANGE, range != 0);
+  raise_flag_sys(flags, F_UNSORTED, unsorted != 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   uint32_t old = 0;
   if (threadIdx.x == 0)
@@ -112,7 +116,7 @@ __device__ __forceinline__ void request_done(uint32_t ticket, const Arrival& a, 
     const uint32_t top = __hip_atomic_fetch_add(a.ctr + kArriveShards * kArriveStride, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
     // no fence before the word: every block's flags were made visible before
-    // its arrival was counted (flag_fence), and the host reads nothing else
+    // its arrival was counted (raise_flag_sys), and the host reads nothing else
     // (a system-scope fence here wrote back the XCD's L2 — every dirty store
     // line of the apply — before the host could learn of the completion)
     if (top == a.top_last) __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
