@@ -4,6 +4,8 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -316,8 +318,74 @@ psg_comm* CreateComm(int group) {
 
 }  // namespace device
 
+namespace {
+// A persistent pool for large host copies (vector -> SVector, staging blocks).
+// Spawning the helper threads per call cost more than the copy it split: a
+// 16 MiB staging chunk copied by 4 fresh threads spent ~25 us on thread
+// creation and join alone.  One job at a time; the caller runs part 0 and
+// the workers take the rest by an atomic ticket.  Never destroyed: its
+// threads may still be parked when static destructors run.
+class CopyPool {
+ public:
+  explicit CopyPool(int nthreads) {
+    for (int i = 0; i < nthreads; ++i) std::thread([this] { Work(); }).detach();
+  }
+  void Run(char* dst, const char* src, size_t bytes, int parts, size_t chunk) {
+    std::lock_guard<std::mutex> job_lk(job_mu_);
+    {
+      // a worker still in Drain from the last job may take a ticket of this
+      // one as soon as next_ is reset: publish everything else first
+      std::lock_guard<std::mutex> lk(mu_);
+      left_.store(parts, std::memory_order_relaxed);
+      dst_ = dst;
+      src_ = src;
+      bytes_ = bytes;
+      chunk_ = chunk;
+      parts_ = parts;
+      next_.store(1, std::memory_order_release);
+      ++gen_;
+    }
+    cv_.notify_all();
+    Part(0);
+    Drain();
+    // the workers may still be taking tickets past the end: wait for all parts
+    while (left_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+  }
+
+ private:
+  void Part(int i) {
+    const size_t off = chunk_ * (size_t)i;
+    if (off < bytes_) std::memcpy(dst_ + off, src_ + off, std::min(chunk_, bytes_ - off));
+    left_.fetch_sub(1, std::memory_order_acq_rel);
+  }
+  void Drain() {
+    for (int i; (i = next_.fetch_add(1, std::memory_order_acq_rel)) < parts_;) Part(i);
+  }
+  void Work() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      Drain();
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_;
+  uint64_t gen_ = 0;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t bytes_ = 0, chunk_ = 0;
+  int parts_ = 0;
+  std::atomic<int> next_{0}, left_{0};
+};
+}  // namespace
+
 void HostCopy(void* dst, const void* src, size_t bytes) {
-  constexpr size_t kSplit = size_t(16) << 20;
+  constexpr size_t kSplit = size_t(4) << 20;  // below this one memcpy
+  constexpr size_t kPart = size_t(1) << 20;   // smallest part handed to a worker
   static const int nthreads = [] {
     unsigned hc = std::thread::hardware_concurrency();
     const char* e = std::getenv("PS_COPY_THREADS");
@@ -328,17 +396,10 @@ void HostCopy(void* dst, const void* src, size_t bytes) {
     std::memcpy(dst, src, bytes);
     return;
   }
-  const int parts = (int)std::min<size_t>((size_t)nthreads, bytes / (kSplit / 4));
+  static CopyPool* pool = new CopyPool(nthreads - 1);
+  const int parts = (int)std::min<size_t>((size_t)nthreads, bytes / kPart);
   const size_t chunk = (bytes / parts + 4095) & ~size_t(4095);
-  std::vector<std::thread> ts;
-  for (int i = 1; i < parts; ++i) {
-    const size_t off = chunk * i;
-    if (off >= bytes) break;
-    const size_t len = std::min(chunk, bytes - off);
-    ts.emplace_back([=] { std::memcpy((char*)dst + off, (const char*)src + off, len); });
-  }
-  std::memcpy(dst, src, std::min(chunk, bytes));
-  for (auto& t : ts) t.join();
+  pool->Run((char*)dst, (const char*)src, bytes, parts, chunk);
 }
 
 }  // namespace ps
