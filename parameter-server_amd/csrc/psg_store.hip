@@ -48,13 +48,14 @@ constexpr int kTile = 1024;  // request keys per block tile (4 per lane)
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
 // Request flags live in pinned host memory that the kernels write directly
-// (one plain store of 1 per wave that saw the condition — idempotent, no
-// atomics), so a request needs no flag reset launch and no flag copy: the
-// host zeroes them before the launch and reads them after the stream sync.
+// (one store of 1 per wave that saw the condition — idempotent, no atomics),
+// so a request needs no flag reset launch and no flag copy: the host zeroes
+// them before the launch and reads them once the request's completion word
+// has appeared (written by the stream, read_flags, or by k_resolve_apply
+// itself, request_done).
 // F_WINMISS: a cached window did not match its tile (searched inline).
 enum { F_MISSING = 0, F_WINMISS = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
-// the host-memory word after the flags that the stream's completion write
-// targets (read_flags); never zeroed by reset_flags
+// the host-memory completion word after the flags; never zeroed by reset_flags
 constexpr int kDoneWord = F_NFLAGS;
 
 __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
