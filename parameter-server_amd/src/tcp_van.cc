@@ -51,6 +51,7 @@
 
 #include "internal/Env.h"
 #include "internal/PostOffice.h"
+#include "internal/customer.h"
 #include "internal/device.h"
 #include "internal/shm_pool.h"
 
@@ -86,6 +87,23 @@ bool ReadAll(int fd, void* buf, size_t n) {
     n -= (size_t)r;
   }
   return true;
+}
+
+// Before a connection's reader blocks in recv for the next message, poll the
+// socket for up to PS_SPIN_US (default 50 us, the spin of the request queues,
+// internal/customer.h): a request round trip crosses the socket twice, and a
+// blocked reader's wake-up costs more than a loopback hop.
+void SpinUntilReadable(int fd) {
+  const int us = SpinMicros();
+  if (us <= 0) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  char c;
+  for (int i = 0;; ++i) {
+    const ssize_t r = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    if (r > 0 || r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) return;
+    if ((i & 7) == 7 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us)) return;
+    __builtin_ia32_pause();
+  }
 }
 
 void Tune(int fd) {
@@ -842,6 +860,7 @@ void TcpVan::ReadLoop(int fd) {
   bool said_goodbye = false;
   while (true) {
     WireHeader wh;
+    SpinUntilReadable(fd);
     if (!ReadAll(fd, &wh, sizeof(wh))) break;
     if (wh.magic != kMagic) {
       LOG(ERROR) << "bad frame header from node " << peer << "; closing the connection";
