@@ -4,7 +4,9 @@
 // detach-on-growth (SliceTest, :411-462), resize/fill, reinterpreting views,
 // FindRange.  Plain program (no PS node): exits non-zero on a failed CHECK.
 #include <cstdio>
+#include <cstdint>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "ps/svector.h"
@@ -96,6 +98,19 @@ int main() {
     ps::Range r = ps::FindRange<uint64_t>(k, 4, 8);
     CHECK_EQ(r.begin, 1u);
     CHECK_EQ(r.end, 3u);
+  }
+  {  // large copies go through the pooled multi-threaded HostCopy: contents
+     // exact, from several threads at once, sizes not multiples of a part
+    auto check_big = [](size_t n, uint32_t seed) {
+      std::vector<uint32_t> v(n);
+      for (size_t i = 0; i < n; ++i) v[i] = (uint32_t)(i * 2654435761u) ^ seed;
+      SVector<uint32_t> s(v);
+      for (size_t i = 0; i < n; ++i) CHECK_EQ(s[i], v[i]) << "at " << i;
+    };
+    check_big((size_t(24) << 20) / 4 + 12345, 7);
+    std::vector<std::thread> ts;
+    for (uint32_t t = 0; t < 4; ++t) ts.emplace_back([&, t] { for (int r = 0; r < 3; ++r) check_big((size_t(9) << 20) + 777 * t, t * 100 + r); });
+    for (auto& t : ts) t.join();
   }
   std::printf("svector ok\n");
   return 0;
