@@ -74,6 +74,9 @@ struct Meta {
   bool pull = false;
   bool simple_app = false;
   bool hbm_handle = false;     // a reply from a server whose handle takes HBM frames
+  // request: a Pull whose frame 1 is the caller's HBM output slice (the server
+  // may write the values there); reply: it did, and carries no values
+  bool direct_reply = false;
   std::string body;
   std::vector<DataType> data_type;
   Control control;

@@ -126,6 +126,16 @@ inline uint64_t KeyListHash(const Key* keys, size_t n) {
   }
   return seed;
 }
+
+/* ZPull offers the servers its HBM output (Meta::direct_reply); PS_DIRECT_REPLY=0
+ * turns the offer off (A/B): every reply is then merged by psg_merge. */
+inline bool DirectReplyOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_DIRECT_REPLY");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 }  // namespace detail
 
 template <typename Value>
@@ -217,7 +227,13 @@ class KVWorker : public SimpleApp {
     Data kvs;
     kvs.keys = keys;
     kvs.priority = priority;
-    Send(ts, false, true, cmd, kvs);
+    // HBM keys and a sized HBM output, no lens: offer each server its slice of
+    // the output (the request's vals frame), so a handle that can write its
+    // reply there does, and the merge copy disappears (detail::DirectReply)
+    const bool direct = vals && lens == nullptr && keys.on_device() && keys.size() && vals->on_device() &&
+                        vals->size() && vals->size() % keys.size() == 0 && detail::DirectReplyOn();
+    if (direct) kvs.vals = *vals;
+    Send(ts, false, true, cmd, kvs, direct);
     return ts;
   }
   int ZPushPull(const SVector<Key>& keys, const SVector<Value>& vals, SVector<Value>* outs,
@@ -242,6 +258,7 @@ class KVWorker : public SimpleApp {
   struct Reply {
     Data kv;
     int sender;
+    bool direct = false;  // the server wrote the values into the output in place
   };
   // servers whose replies said their handle takes HBM frames
   void NoteHbmServer(int sender) {
@@ -264,7 +281,7 @@ class KVWorker : public SimpleApp {
     callbacks_[timestamp] = cb;
   }
   void RunCallback(int timestamp);
-  void Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs);
+  void Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct = false);
   void OnReceive(const Message& msg) override;
   void DefaultSlicer(Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced);
   template <typename C, typename D>
@@ -325,6 +342,23 @@ class KVServer : public SimpleApp {
   std::atomic<bool> device_frames_{false};
   std::mutex handle_mu_;
   std::condition_variable handle_cv_;
+  // the output slice a direct-reply Pull offers while its handle runs (the
+  // customer thread runs one handle at a time), and whether the handle took it
+  SVector<Value> direct_out_;
+  int direct_ts_ = -1, direct_sender_ = -1;
+  bool direct_taken_ = false;
+
+ public:
+  /* For a handle that answers a Pull from HBM: the caller's output slice for
+   * this request's values when the worker offered one of n values (ZPull
+   * with HBM keys and a sized HBM output), else an empty SVector.  A handle
+   * that takes it must write the reply values there (ordered before its
+   * Response) and then Response with keys and no values. */
+  SVector<Value> TakeDirectOut(size_t n) {
+    if (direct_out_.size() != n || !direct_out_.on_device()) return SVector<Value>();
+    direct_taken_ = true;
+    return direct_out_;
+  }
 };
 
 /* The default handle (KVApp.h:433-458): `store[key] += val` for a push,
@@ -373,6 +407,7 @@ struct KVServerDefaultHandle {
     const int flags = (req_meta.push ? PSG_PUSH : 0) | (req_meta.pull ? PSG_PULL : 0);
     psg_stream s = device::ThreadStream();
     SVector<Value> dout;
+    bool direct = false;
     if (state->key_cache && n == 1 && flags) {
       // a cached list named by its hash (LRServer.h:129-135)
       Key h = 0;
@@ -386,7 +421,7 @@ struct KVServerDefaultHandle {
       Refresh(c, s);
       SVector<Value> dvals;
       if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
-      if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
+      if (req_meta.pull) dout = PullOutput(server, n, dev, &direct);
       device::Check(psg_store_handle_slots(state->store, flags, c.slots.data(), dvals.data(), dout.data(), n, s),
                     "psg_store_handle_slots");
       device::Check(psg_stream_sync(s), "psg_stream_sync");
@@ -395,7 +430,7 @@ struct KVServerDefaultHandle {
       SVector<Key> dkeys = detail::ToDeviceAsync(req_data.keys, dev);
       SVector<Value> dvals;
       if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
-      if (req_meta.pull) dout = SVector<Value>::OnDevice(n, dev);
+      if (req_meta.pull) dout = PullOutput(server, n, dev, &direct);
       device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
                     "psg_store_handle");
       // psg_store_handle returns once the request's keys and vals are no longer
@@ -408,7 +443,8 @@ struct KVServerDefaultHandle {
     }
     if (req_meta.pull) {
       res.keys = req_data.keys;
-      res.vals = on_dev ? dout : detail::ToHost(dout);
+      // written into the worker's output in place (TakeDirectOut): no values
+      if (!direct) res.vals = on_dev ? dout : detail::ToHost(dout);
     }
     server->Response(req_meta, res);
   }
@@ -434,6 +470,14 @@ struct KVServerDefaultHandle {
     return info.size;
   }
   // cache a full list under its hash (LRServer.h:136-141: the first one wins)
+  // a Pull's output: the worker's own slice when it offered one of n values
+  // (written in place: no reply frame, no merge), else a fresh HBM array
+  static SVector<Value> PullOutput(KVServer<Value>* server, size_t n, int dev, bool* direct) {
+    SVector<Value> d = server->TakeDirectOut(n);
+    *direct = !d.empty();
+    return *direct ? d : SVector<Value>::OnDevice(n, dev);
+  }
+
   void Remember(const SVector<Key>& dkeys, uint64_t host_hash, psg_stream s) {
     const size_t n = dkeys.size();
     uint64_t h = host_hash;
@@ -484,7 +528,20 @@ void KVServer<Value>::OnReceive(const Message& msg) {
   CHECK(installed) << "no request handle installed 30 s after the first request";
   KVPairs<Value> data;
   const size_t n = msg.data.size();
-  if (n) {
+  direct_out_ = SVector<Value>();
+  direct_taken_ = false;
+  if (n && msg.meta.direct_reply && meta.pull && !meta.push) {
+    // frame 1 is not request values: it is where this Pull's values may go
+    CHECK_EQ(n, (size_t)2);
+    data.keys = msg.data[0];
+    if (device_frames) {
+      direct_out_ = msg.data[1];
+      direct_ts_ = meta.timestamp;
+      direct_sender_ = meta.sender;
+    } else {
+      data.keys = detail::ToHost(data.keys);
+    }
+  } else if (n) {
     CHECK_GE(n, (size_t)2);
     data.keys = msg.data[0];
     data.vals = msg.data[1];
@@ -501,6 +558,8 @@ void KVServer<Value>::OnReceive(const Message& msg) {
   }
   // called in place: a handle keeps its state across requests (KVApp.h:457)
   request_handle_(meta, data, this);
+  direct_out_ = SVector<Value>();
+  direct_taken_ = false;
 }
 
 template <typename Value>
@@ -516,6 +575,9 @@ void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
   msg.meta.receiver = req.sender;
   // tells the worker that HBM frames reach this handle without a copy back
   msg.meta.hbm_handle = device_frames_.load();
+  // the handle wrote this Pull's values into the worker's output in place
+  msg.meta.direct_reply = direct_taken_ && req.timestamp == direct_ts_ && req.sender == direct_sender_;
+  if (msg.meta.direct_reply) CHECK(res.vals.empty()) << "a direct reply carries no values";
   if (res.keys.size()) {
     msg.AddData(res.keys);
     msg.AddData(res.vals);
@@ -590,7 +652,7 @@ void KVWorker<Value>::DefaultSlicer(Data& send, const std::vector<Range>& ranges
 }
 
 template <typename Value>
-void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs) {
+void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct) {
   SlicedKVs sliced;
   slicer_(const_cast<Data&>(kvs), PostOffice::Get()->GetServerRanges(), &sliced);
   int skipped = 0;
@@ -611,6 +673,7 @@ void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const D
     msg.meta.timestamp = timestamp;
     msg.meta.receiver = PostOffice::ServerRankToID((int)i);
     msg.meta.priority = kvs.priority;
+    msg.meta.direct_reply = direct;
     const auto& kv = s.second;
     if (kv.keys.size()) {
       msg.AddData(kv.keys);
@@ -636,6 +699,7 @@ void KVWorker<Value>::OnReceive(const Message& msg) {
     r.kv.vals = msg.data[1];
     if (msg.data.size() > 2) r.kv.lens = msg.data[2];
     r.sender = msg.meta.sender;
+    r.direct = msg.meta.direct_reply;
     std::lock_guard<std::mutex> lk(mu_);
     recv_kvs_[ts].push_back(std::move(r));
   }
@@ -682,7 +746,7 @@ template <typename Value>
 template <typename C, typename D>
 void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kvs, C* vals, D* lens) {
   size_t total_key = 0, total_val = 0;
-  int ndev = 0;
+  int ndev = 0, ndirect = 0;
   for (const auto& r : kvs) {
     const auto& s = r.kv;
     if (!s.keys.on_device() && !keys.on_device() && s.keys.size()) {
@@ -691,11 +755,18 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
     }
     if (lens) CHECK_EQ(s.lens.size(), s.keys.size());
     total_key += s.keys.size();
+    if (r.direct) {
+      // written in place: its slice of the output, keys x values per key
+      CHECK(!lens && vals && keys.size()) << "a direct reply needs a sized output and no lens";
+      total_val += s.keys.size() * (vals->size() / keys.size());
+      ++ndirect;
+      continue;
+    }
     total_val += s.vals.size();
     ndev += s.vals.on_device() ? 1 : 0;
   }
   CHECK_EQ(total_key, keys.size()) << "lost some servers?";
-  CHECK(ndev == 0 || ndev == (int)kvs.size()) << "pull replies mix host and HBM frames";
+  CHECK(ndev == 0 || ndev + ndirect == (int)kvs.size()) << "pull replies mix host and HBM frames";
   // order the replies by their first key (KVApp.h:694-696); replies whose keys
   // are in HBM are ordered by server rank, which the default ranges make the same
   if (!keys.on_device()) {
@@ -713,7 +784,9 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
   } else {
     CHECK_EQ(vals->size(), total_val);
   }
-  if (ndev == 0 && out_dev < 0) {
+  if (ndirect == (int)kvs.size()) {
+    // every server wrote its values in place: nothing to merge
+  } else if (ndev == 0 && out_dev < 0) {
     Value* p = vals->data();
     for (const auto& r : kvs) {
       if (r.kv.vals.size()) HostCopy(p, r.kv.vals.data(), r.kv.vals.size() * sizeof(Value));
@@ -723,7 +796,14 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
     std::vector<psg_segment> segs;
     std::vector<SVector<Value>> staged;  // host replies going to an HBM output
     const int my_dev = PostOffice::Get()->device();
+    const size_t per_key = keys.size() ? total_val / keys.size() : 0;
+    std::vector<uint64_t> offs;  // where each segment goes in the output
+    uint64_t done_vals = 0;      // values of the replies before j (direct ones included)
     for (size_t j = 0; j < kvs.size(); ++j) {
+      if (kvs[j].direct) {
+        done_vals += kvs[j].kv.keys.size() * per_key;
+        continue;
+      }
       const SVector<Value>& v = kvs[j].kv.vals;
       const Value* src = v.data();
       if (!v.on_device() && v.size()) {
@@ -731,9 +811,17 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
         src = staged.back().data();
       }
       segs.push_back(psg_segment{src, v.size(), (uint64_t)j});  // j: already in order
+      offs.push_back(done_vals);
+      done_vals += v.size();
     }
-    if (out_dev >= 0) {
+    if (out_dev >= 0 && ndirect == 0) {
       device::Merge(&segs, sizeof(Value), vals->data(), total_val);
+    } else if (out_dev >= 0) {
+      // some servers wrote in place: copy the other replies to their slices
+      for (size_t t = 0; t < segs.size(); ++t) {
+        std::vector<psg_segment> one{segs[t]};
+        device::Merge(&one, sizeof(Value), vals->data() + offs[t], segs[t].count);
+      }
     } else {
       SVector<Value> tmp = SVector<Value>::OnDevice(total_val, my_dev);
       device::Merge(&segs, sizeof(Value), tmp.data(), total_val);

@@ -189,7 +189,8 @@ void PutMeta(Writer& w, const Meta& m) {
   w.pod<int32_t>(m.timestamp);
   w.pod<int32_t>(m.sender);
   w.pod<int32_t>(m.receiver);
-  w.pod<uint8_t>((uint8_t)(m.request | (m.push << 1) | (m.pull << 2) | (m.simple_app << 3) | (m.hbm_handle << 4)));
+  w.pod<uint8_t>((uint8_t)(m.request | (m.push << 1) | (m.pull << 2) | (m.simple_app << 3) | (m.hbm_handle << 4) |
+                           (m.direct_reply << 5)));
   w.str(m.body);
   w.pod<uint32_t>((uint32_t)m.data_type.size());
   for (DataType t : m.data_type) w.pod<int32_t>((int32_t)t);
@@ -216,6 +217,7 @@ Meta GetMeta(Reader& r) {
   m.pull = (f >> 2) & 1;
   m.simple_app = (f >> 3) & 1;
   m.hbm_handle = (f >> 4) & 1;
+  m.direct_reply = (f >> 5) & 1;
   m.body = r.str();
   const uint32_t nt = r.pod<uint32_t>();
   for (uint32_t i = 0; i < nt; ++i) m.data_type.push_back((DataType)r.pod<int32_t>());

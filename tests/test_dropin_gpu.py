@@ -100,11 +100,15 @@ def test_default_handle_key_cache_end_to_end(nw):
     assert len(lines) == nw and all(l["key_cache"] == 1 for l in lines)
 
 
-@pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
-def test_device_frames_end_to_end(ns, nw):
+@pytest.mark.parametrize("ns,nw,direct", [(1, 1, True), (2, 2, True), (2, 2, False)])
+def test_device_frames_end_to_end(ns, nw, direct):
+    """HBM ZPush / ZPull / ZPushPull through the C++ API, every value checked.
+    ZPull offers each server its slice of the caller's HBM output, and the
+    default handle writes its reply there (no reply frame, no merge);
+    PS_DIRECT_REPLY=0 keeps the merged replies."""
     exe = os.path.join(BIN, "kv_cluster_device")
     _need(exe)
-    r = run(exe, "-ns", ns, "-nw", nw, 200000, 20)
+    r = run(exe, "-ns", ns, "-nw", nw, 200000, 20, env=None if direct else {"PS_DIRECT_REPLY": "0"})
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == nw
@@ -161,8 +165,9 @@ def test_reference_test_my_processes():
 @pytest.mark.parametrize("ns,nw", [(1, 1), (2, 2)])
 def test_device_frames_across_processes(ns, nw):
     """ZPush / ZPull of HBM SVectors between processes: the server kernels read
-    the workers' keys and values through hipIpc mappings, the pull replies
-    (server HBM) are merged in place by the worker, and the echoed key frames
+    the workers' keys and values through hipIpc mappings and write each Pull's
+    values straight into the worker's output through the mapping of the slice
+    the worker offered (no reply frame, no merge), and the echoed key frames
     resolve to the worker's own arrays."""
     exe = os.path.join(BIN, "kv_cluster_device")
     _need(exe)
