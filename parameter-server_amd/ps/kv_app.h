@@ -344,16 +344,18 @@ class KVServer : public SimpleApp {
   std::condition_variable handle_cv_;
   // the output slice a direct-reply Pull offers while its handle runs (the
   // customer thread runs one handle at a time), and whether the handle took it
+  // (atomics: a handle may answer a deferred request from another thread)
   SVector<Value> direct_out_;
-  int direct_ts_ = -1, direct_sender_ = -1;
-  bool direct_taken_ = false;
+  std::atomic<int> direct_ts_{-1}, direct_sender_{-1};
+  std::atomic<bool> direct_taken_{false};
 
  public:
   /* For a handle that answers a Pull from HBM: the caller's output slice for
    * this request's values when the worker offered one of n values (ZPull
    * with HBM keys and a sized HBM output), else an empty SVector.  A handle
    * that takes it must write the reply values there (ordered before its
-   * Response) and then Response with keys and no values. */
+   * Response) and then Response with keys and no values, from inside the
+   * handle (a deferred Response is not marked as written in place). */
   SVector<Value> TakeDirectOut(size_t n) {
     if (direct_out_.size() != n || !direct_out_.on_device()) return SVector<Value>();
     direct_taken_ = true;
@@ -576,7 +578,7 @@ void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
   // tells the worker that HBM frames reach this handle without a copy back
   msg.meta.hbm_handle = device_frames_.load();
   // the handle wrote this Pull's values into the worker's output in place
-  msg.meta.direct_reply = direct_taken_ && req.timestamp == direct_ts_ && req.sender == direct_sender_;
+  msg.meta.direct_reply = direct_taken_.load() && req.timestamp == direct_ts_.load() && req.sender == direct_sender_.load();
   if (msg.meta.direct_reply) CHECK(res.vals.empty()) << "a direct reply carries no values";
   if (res.keys.size()) {
     msg.AddData(res.keys);
