@@ -925,7 +925,7 @@ def main(argv=None) -> None:
     ap.add_argument("--keys", type=int, default=None, help="values per worker (default by workload)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--check", type=int, default=1)
-    ap.add_argument("--event-every", type=int, default=5,
+    ap.add_argument("--event-every", type=int, default=10,
                     help="record the kernel-timing HIP events on every n-th timed step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe256", action="store_true")
