@@ -178,6 +178,19 @@ void EnableAllPeerAccess() {
 void CopySync(void* dst, const void* src, size_t bytes, int kind) {
   if (!bytes) return;
   psg_stream s = ThreadStream();
+  // a few bytes out of HBM (a hashed key list's one key): through a pinned
+  // per-thread word, not a pageable destination the runtime stages itself
+  constexpr size_t kSmall = 64;
+  thread_local void* small = nullptr;
+  if (kind == 1 && bytes <= kSmall) {
+    if (!small && psg_host_alloc(&small, kSmall) != PSG_OK) small = nullptr;
+    if (small) {
+      Check(psg_memcpy(small, src, bytes, kind, s), "psg_memcpy");
+      Check(psg_stream_sync(s), "psg_stream_sync");
+      std::memcpy(dst, small, bytes);
+      return;
+    }
+  }
   Check(psg_memcpy(dst, src, bytes, kind, s), "psg_memcpy");
   Check(psg_stream_sync(s), "psg_stream_sync");
 }
