@@ -245,7 +245,10 @@ class KVWorker : public SimpleApp {
     kvs.vals = vals;
     kvs.priority = priority;
     if (lens) kvs.lens = *lens;  // the reference forwards the output lens (KVApp.h:287-288)
-    Send(ts, true, true, cmd, kvs);
+    // as ZPull: offer each server its slice of the HBM output (outs mirrors vals)
+    const bool direct = outs && lens == nullptr && keys.on_device() && keys.size() && outs->on_device() &&
+                        outs->size() == vals.size() && vals.on_device() && detail::DirectReplyOn();
+    Send(ts, true, true, cmd, kvs, direct, direct ? outs : nullptr);
     return ts;
   }
 
@@ -281,7 +284,8 @@ class KVWorker : public SimpleApp {
     callbacks_[timestamp] = cb;
   }
   void RunCallback(int timestamp);
-  void Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct = false);
+  void Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct = false,
+            const SVector<Value>* outs = nullptr);
   void OnReceive(const Message& msg) override;
   void DefaultSlicer(Data& send, const std::vector<Range>& ranges, SlicedKVs* sliced);
   template <typename C, typename D>
@@ -532,16 +536,19 @@ void KVServer<Value>::OnReceive(const Message& msg) {
   const size_t n = msg.data.size();
   direct_out_ = SVector<Value>();
   direct_taken_ = false;
-  if (n && msg.meta.direct_reply && meta.pull && !meta.push) {
-    // frame 1 is not request values: it is where this Pull's values may go
-    CHECK_EQ(n, (size_t)2);
+  if (n && msg.meta.direct_reply && meta.pull) {
+    // the last frame is not request data: it is where this Pull's (or
+    // PushPull's) values may go — [keys, out] or [keys, vals, out]
+    CHECK_EQ(n, meta.push ? (size_t)3 : (size_t)2);
     data.keys = msg.data[0];
+    if (meta.push) data.vals = msg.data[1];
     if (device_frames) {
-      direct_out_ = msg.data[1];
+      direct_out_ = msg.data[n - 1];
       direct_ts_ = meta.timestamp;
       direct_sender_ = meta.sender;
     } else {
       data.keys = detail::ToHost(data.keys);
+      data.vals = detail::ToHost(data.vals);
     }
   } else if (n) {
     CHECK_GE(n, (size_t)2);
@@ -654,7 +661,8 @@ void KVWorker<Value>::DefaultSlicer(Data& send, const std::vector<Range>& ranges
 }
 
 template <typename Value>
-void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct) {
+void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct,
+                           const SVector<Value>* outs) {
   SlicedKVs sliced;
   slicer_(const_cast<Data&>(kvs), PostOffice::Get()->GetServerRanges(), &sliced);
   int skipped = 0;
@@ -677,10 +685,25 @@ void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const D
     msg.meta.priority = kvs.priority;
     msg.meta.direct_reply = direct;
     const auto& kv = s.second;
+    SVector<Value> out_slice;
+    if (direct && outs) {
+      // a PushPull: the output slice at this server's values' offset, found
+      // from where its vals slice sits in the request (a slicer that copied
+      // the values instead of slicing them gets no offer)
+      const Value* base = kvs.vals.data();
+      const Value* v = kv.vals.data();
+      if (kv.vals.size() && v >= base && v + kv.vals.size() <= base + kvs.vals.size()) {
+        const size_t off = (size_t)(v - base);
+        out_slice = outs->Slice(off, off + kv.vals.size());
+      } else {
+        msg.meta.direct_reply = false;
+      }
+    }
     if (kv.keys.size()) {
       msg.AddData(kv.keys);
       msg.AddData(kv.vals);
       if (kv.lens.size()) msg.AddData(kv.lens);
+      if (msg.meta.direct_reply && outs) msg.AddData(out_slice);
     }
     PostOffice::Get()->van()->Send(msg);
   }
