@@ -9,7 +9,8 @@
 // KVServerDefaultHandle<float> (HBM store).  Checks the test_kv_app.cpp
 // expectations (50 pushes -> 50 * vals, 50 push-pulls -> 100 * vals) and
 // prints one JSON line of timings per worker:
-//   {"rank":r,"n":N,"device_push_ms":..,"device_pull_ms":..,"host_push_ms":..,"host_pull_ms":..}
+//   {"rank":r,"n":N,"device_push_ms":..,"device_pull_ms":..,"device_pushpull_ms":..,
+//    "host_push_ms":..,"host_pull_ms":..}
 // With key_cache = 1 the server runs KVServerDefaultHandle<float>(true) and the
 // timed requests carry ONE key, the hash of the list the untimed first
 // request sent (the LR key-cache protocol, LRServer.h:127-142 / LRWorker.h:
@@ -76,7 +77,9 @@ int main(int argc, char* argv[]) {
     std::vector<float> got(num);
     device::CopySync(got.data(), dout.data(), num * sizeof(float), 1);
     for (long i = 0; i < num; ++i) CHECK_EQ(got[i], hvals[i] * (repeat + 1)) << "device path, i=" << i;
+    t0 = clk::now();
     for (int r = 0; r < repeat; ++r) kv.Wait(kv.ZPushPull(dkeys, dvals, &dout));
+    double dpushpull = ms_since(t0) / repeat;
     device::CopySync(got.data(), dout.data(), num * sizeof(float), 1);
     for (long i = 0; i < num; ++i)
       CHECK_EQ(got[i], hvals[i] * (2 * repeat + 1)) << "device push-pull, i=" << i;
@@ -108,8 +111,9 @@ int main(int argc, char* argv[]) {
       CHECK_EQ(outs[i], hvals[i] * (2 * repeat + 4)) << "host push-pull, i=" << i;
 
     std::printf("{\"rank\": %d, \"n\": %ld, \"servers\": %d, \"key_cache\": %d, \"device_push_ms\": %.4f, "
-                "\"device_pull_ms\": %.4f, \"host_push_ms\": %.4f, \"host_pull_ms\": %.4f}\n",
-                rank, num, NumServers(), (int)key_cache, dpush, dpull, hpush, hpull);
+                "\"device_pull_ms\": %.4f, \"device_pushpull_ms\": %.4f, \"host_push_ms\": %.4f, "
+                "\"host_pull_ms\": %.4f}\n",
+                rank, num, NumServers(), (int)key_cache, dpush, dpull, dpushpull, hpush, hpull);
     std::fflush(stdout);
   }
   Finalize(0, true);
