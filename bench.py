@@ -86,6 +86,7 @@ class GpuBackend:
         self.stream = psg.Stream()
         self.comm = None
         self.xgmi = None
+        self.store = None
         self.mode = "rccl"  # "rccl" (RS + AG, or pipelined when fused) or "xgmi"
         self.fused = False
         self.nbuckets = 1
@@ -282,7 +283,10 @@ class GpuBackend:
             # one server: the slice is the whole request (KVWorker's DefaultSlicer
             # skips the kernel for a single range; the store's range check covers it)
             if self.comm is None:
-                self.store.handle(self.p.PUSH, self.keys, self.vals, None, self.L, stream=self.stream)
+                # launched without waiting for its completion word: the next
+                # request queues behind it on the stream (psg_store_handle_async);
+                # sync() reaps them all and raises any failure
+                self.store.handle_async(self.p.PUSH, self.keys, self.vals, None, self.L, stream=self.stream)
             else:
                 self.comm.push_keyed(self.store, self.keys, self.vals, self.L, self._key_pos(), self.stream)
         elif self.comm is None:
@@ -321,7 +325,7 @@ class GpuBackend:
             self.store.handle_slots(self.p.PULL, self.slots, None, self.out, self.L, stream=self.stream)
         elif self.keyed:
             if self.comm is None:
-                self.store.handle(self.p.PULL, self.keys, None, self.out, self.L, stream=self.stream)
+                self.store.handle_async(self.p.PULL, self.keys, None, self.out, self.L, stream=self.stream)
             else:
                 self.comm.pull_keyed(self.store, self.keys, self.out, self.L, self._key_pos(), self.stream)
         elif self.comm is None:
@@ -513,6 +517,8 @@ class GpuBackend:
         return a.elapsed_ms(b)
 
     def sync(self):
+        if self.keyed and self.store is not None:
+            self.store.wait()  # the keyed requests in flight, their follow-ups and failures
         self.stream.sync()
         self.p.device_sync()
 
@@ -813,9 +819,20 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                                    "k_dense_vec<PUSH> on the shard after the reduce-scatter", vb)
     else:
         res["roofline"] = None
+    if world == 1 and wl == "dense" and res.get("roofline"):
+        # the 64 M store (256 MiB) stays in the 256 MiB Infinity Cache between
+        # the Push and the Pull, so this fraction is IC-assisted, not pure HBM;
+        # the pure-HBM figure is the 256 M north-star probe below
+        store_mib = vb * blk / 2**20
+        res["roofline"]["infinity_cache_assisted"] = store_mib <= 256
+        res["roofline"]["store_mib"] = round(store_mib, 1)
     if (world == 1 and wl == "dense" and hasattr(backend, "probe_256m")
             and not getattr(args, "no_probe256", False)):
         res["push256_roofline"] = backend.probe_256m()
+        if res.get("roofline"):
+            res["roofline"]["hbm_only_frac_256m"] = res["push256_roofline"]["push_frac"]
+            res["roofline"]["hbm_only_note"] = ("push256_roofline: the same Push kernel on a 1 GiB store "
+                                                "(256 M floats), past the Infinity Cache")
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)
     res["runtime_libs"] = mapped_runtime_libs()
@@ -826,7 +843,7 @@ def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed PMC summaries (tools/pmc_summary.py):
     # the one measured on this kernel at these algorithmic bytes, if any
-    traffic = None
+    traffic, source = None, None
     import glob
     for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
@@ -836,6 +853,7 @@ def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
         names = [k.split("<")[0].strip() for k in str(d.get("kernel", "")).split("|")]
         if d.get("alg_bytes_per_launch") == alg_bytes and names and all(n in kernel for n in names):
             traffic = d.get("hbm_bytes_per_launch")
+            source = os.path.relpath(pmc, ROOT)
             break
     return {
         "kernel": kernel,
@@ -845,6 +863,10 @@ def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        # traffic is NOT counted in this run: it is the HBM bytes per launch of
+        # the committed rocprofv3 PMC summary (FETCH_SIZE x2 + WRITE_SIZE) of
+        # this kernel at these algorithmic bytes
+        "traffic_source": source,
         "alg_bytes_per_launch": alg_bytes,
     }
 

@@ -171,28 +171,60 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  *   for i < n:  if (flags & PSG_PUSH) store[key_i] += vals[i];
  *               if (flags & PSG_PULL) out[i] = store[key_i];   (post-update)
  * keys == NULL means the consecutive keys first_key, first_key + 1, ...
- * (dense request: no key array travels).  Keys must be strictly ascending
- * (KVPairs contract, KVApp.h:23); a PULL of an absent key inserts it with 0.
- * A DENSE store accepts only keys inside [key_begin, key_begin + capacity).
- * A request that breaks either rule fails (PSG_ERR_INVALID / PSG_ERR_RANGE)
- * and leaves the store unchanged; the contents of out are then unspecified.
+ * (dense request: no key array travels).  Keys may come in any order and may
+ * repeat, as the reference's loop allows: each occurrence adds in arrival
+ * order and a PushPull answers each occurrence with the running value.
+ * Strictly ascending keys (the KVPairs contract, KVApp.h:23) take the fused
+ * streaming kernels; any other request takes the order-preserving path (a
+ * stable device sort by slot, then one lane per key walking its occurrences),
+ * with the same result bit for bit.  An absent key is inserted with 0
+ * (operator[], KVApp.h:449/452).  A key outside the store's range (a DENSE
+ * store: outside [key_begin, key_begin + capacity)) fails the request
+ * (PSG_ERR_RANGE) and leaves the store unchanged; out is then unspecified.
  * vals/out are device arrays of n elements of the store's dtype.
  * A keyed request (SORTED store, or DENSE with keys) returns once the request
- * has been checked and its keys and vals are no longer read — the caller may
- * reuse them — while its last store and reply writes may still be in flight:
- * work that reads out or the store must be ordered after it on `stream`.  (On
- * the steady SORTED path it waits for a completion word its own kernel
- * writes, not for the stream.)  The store remembers the LDS windows of the last few
- * key arrays it saw (by device pointer and n) and verifies them per tile, so
- * a caller may rewrite a key array in place between requests. */
+ * is complete and its keys and vals are no longer read — the caller may reuse
+ * them — while its last store and reply writes may still be in flight: work
+ * that reads out or the store must be ordered after it on `stream`.  (On the
+ * steady SORTED path it waits for the completion word its own kernel writes,
+ * which also carries the request's flags, not for the stream.)  The store
+ * remembers the LDS windows of the last few key arrays it saw (by device
+ * pointer and n) and verifies them per tile, so a caller may rewrite a key
+ * array in place between requests. */
 int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,
                      uint64_t first_key, const void* vals, void* out, uint64_t n,
                      psg_stream stream);
 
+/* The same request without waiting for it (the server answering a stream of
+ * requests, KVServer::Process, KVApp.h:462-489): a fused keyed request on a
+ * populated SORTED store is launched and *ticket names it; every other request
+ * completes before the call returns (*ticket = 0).  Requests of one store run
+ * in call order.  keys / vals / out must stay untouched until the ticket is
+ * waited for.  A request that needs the host (absent keys to insert, keys out
+ * of order) raises a device word that makes every request launched after it
+ * write nothing; the wait that reaps it inserts the keys, clears the word and
+ * replays those requests, in order — the store sees exactly the call sequence.
+ * psg_store_wait(s, t) completes every request up to ticket t (0: all) and
+ * returns the first failure of those not reported yet.  Every other store call
+ * completes the requests in flight first. */
+int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys,
+                           uint64_t first_key, const void* vals, void* out, uint64_t n,
+                           psg_stream stream, uint64_t* ticket);
+int psg_store_wait(psg_store* s, uint64_t ticket);
+
+/* The stable device radix sort of the order-preserving path (psg_sort.hip),
+ * exported for its parity tests: sorts (keys[i], vals[i]) by bits [0, bits) of
+ * the key, equal keys keeping their order.  In place; synchronous on `stream`'s
+ * order (allocates its scratch stream-ordered). */
+int psg_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t n, int bits, psg_stream stream);
+
 /* Slot cache (LR USE_KEY_CACHING, tests/src/LRServer.h:127-142): resolve a key
  * list to slot indices once, then run requests by slot.  insert != 0 inserts
  * absent keys (value 0) and synchronises the stream; insert == 0 writes
- * UINT32_MAX for absent keys.  Slots stay valid until the next insert. */
+ * UINT32_MAX for absent keys.  Slots stay valid until the next insert.  A
+ * slot list names each key once: its keys must be strictly ascending
+ * (PSG_ERR_INVALID otherwise), since the slot kernels update a slot from one
+ * lane. */
 int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert,
                       uint32_t* slots, psg_stream stream);
 int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots,
@@ -252,10 +284,28 @@ int psg_merge(psg_segment* segs_host, int nsegs, int elem_size, void* dst,
 /* Bytes of the opaque id rank 0 creates and every rank passes to init (two
  * RCCL unique ids: one communicator per direction of psg_comm_push_pull).
  * PSG_COMM_FORCE_COLLECTIVE=1 makes a one-rank comm run the collectives
- * anyway (they degenerate to copies) so the RCCL calls can be tested on one GPU. */
+ * anyway (they degenerate to copies) so the RCCL calls can be tested on one GPU.
+ * psg_comm_init never waits for a missing rank for good: the RCCL inits run on
+ * a helper thread, waited for against PSG_COMM_TIMEOUT_S (default 90 s); when
+ * a rank does not join, init fails with PSG_ERR_COMM on every rank that did
+ * (the reference's Van waits for ADD_NODE the same way, Van.cpp:320-442, but
+ * without a deadline). */
 int psg_comm_id_bytes(void);
 int psg_comm_get_id(void* id_host);
 int psg_comm_init(const void* id_host, int nranks, int rank, psg_comm** out);
+
+/* Host-only plans of the exchanges (no GPU needed): the offsets the RCCL
+ * paths use, exported so the multi-rank CPU rehearsal (tests/test_dist.py)
+ * drives its gloo collectives with the very same numbers.
+ * psg_comm_bucket_plan: the buckets of psg_comm_push_pull over a block of blk
+ * elements — bucket b covers [offs[b], offs[b] + cnts[b]) of every rank's
+ * block; chunks are multiples of 64 elements.  *nb_out = the bucket count
+ * (<= cap, else PSG_ERR_INVALID).
+ * psg_comm_keyed_plan: checks key_pos[nranks+1] as psg_comm_push_keyed /
+ * _pull_keyed do (key_pos[0] = 0, key_pos[nranks] = n, ascending) and returns
+ * the longest segment (the reduce scratch the owner needs). */
+int psg_comm_bucket_plan(uint64_t blk, int nbuckets, uint64_t* offs, uint64_t* cnts, int cap, int* nb_out);
+int psg_comm_keyed_plan(const uint64_t* key_pos_host, int nranks, uint64_t n, uint64_t* maxseg);
 int psg_comm_destroy(psg_comm* c);
 int psg_comm_rank(psg_comm* c, int* rank, int* nranks);
 

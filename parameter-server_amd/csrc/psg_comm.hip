@@ -16,8 +16,13 @@
 // once.  Two communicators keep the two streams' collectives independent.
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "psg_internal.h"
@@ -84,11 +89,14 @@ using namespace psg;
 
 extern "C" {
 
-int psg_comm_id_bytes(void) { return 2 * (int)sizeof(ncclUniqueId); }
+// Two unique ids: one communicator per direction of psg_comm_push_pull.
+constexpr int kCommIds = 2;
+
+int psg_comm_id_bytes(void) { return kCommIds * (int)sizeof(ncclUniqueId); }
 
 int psg_comm_get_id(void* id_host) {
   PSG_REQUIRE(id_host, PSG_ERR_INVALID, "psg_comm_get_id: null out");
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kCommIds; ++k) {
     ncclUniqueId id;
     PSG_NCCL(ncclGetUniqueId(&id));
     memcpy((char*)id_host + k * sizeof(id), &id, sizeof(id));
@@ -96,26 +104,90 @@ int psg_comm_get_id(void* id_host) {
   return PSG_OK;
 }
 
+}  // extern "C"
+
+namespace psg {
+
+// Seconds a communicator's rendezvous may take (PSG_COMM_TIMEOUT_S, default 90).
+static double comm_timeout_s() {
+  const char* e = getenv("PSG_COMM_TIMEOUT_S");
+  const double v = e ? atof(e) : 0.0;
+  return v > 0 ? v : 90.0;
+}
+
+// ncclCommInitRank blocks until every rank of the communicator has joined, and
+// RCCL has no deadline of its own: one rank that never arrives (it died before
+// init, or runs another job) would hang every other rank for good.  (RCCL
+// 2.27's non-blocking config did not help here: ncclCommInitRankConfig with
+// blocking = 0 still blocked in the rendezvous, measured on MI355X with a rank
+// missing.)  So the two inits run on a helper thread and the caller waits for
+// them against a deadline.  On a timeout psg_comm_init fails with PSG_ERR_COMM
+// on this rank — every rank of such a job fails the same way within the
+// deadline — so the caller can fall back (bench.py: the xGMI kernels, agreed by
+// all ranks) or exit with a message instead of hanging.  The helper thread is
+// then abandoned inside RCCL: it owns everything it touches (the job below),
+// and if its peers do turn up later it leaves the communicators it made unused.
+struct CommInitJob {
+  ncclUniqueId ids[kCommIds];
+  int nranks = 0, rank = 0, device = 0;
+  ncclComm_t comm[kCommIds] = {};
+  ncclResult_t r = ncclSuccess;
+  hipError_t e = hipSuccess;
+  bool done = false;
+  std::mutex mu;
+  std::condition_variable cv;
+};
+
+static void comm_init_thread(std::shared_ptr<CommInitJob> j) {
+  ncclResult_t r = ncclSuccess;
+  hipError_t e = hipSetDevice(j->device);  // HIP's current device is per thread
+  ncclComm_t comm[kCommIds] = {};
+  if (e == hipSuccess) {
+    for (int k = 0; k < kCommIds && r == ncclSuccess; ++k) r = ncclCommInitRank(&comm[k], j->nranks, j->ids[k], j->rank);
+    if (r != ncclSuccess)
+      for (int k = 0; k < kCommIds; ++k)
+        if (comm[k]) (void)ncclCommDestroy(comm[k]);
+  }
+  std::lock_guard<std::mutex> lk(j->mu);
+  j->r = r;
+  j->e = e;
+  for (int k = 0; k < kCommIds; ++k) j->comm[k] = r == ncclSuccess ? comm[k] : nullptr;
+  j->done = true;
+  j->cv.notify_all();
+}
+
+}  // namespace psg
+
+extern "C" {
+
 int psg_comm_init(const void* id_host, int nranks, int rank, psg_comm** out) {
   PSG_REQUIRE(id_host && out && nranks > 0 && rank >= 0 && rank < nranks, PSG_ERR_INVALID,
               "psg_comm_init: bad arguments");
   *out = nullptr;
+  auto job = std::make_shared<CommInitJob>();
+  for (int k = 0; k < kCommIds; ++k) memcpy(&job->ids[k], (const char*)id_host + k * sizeof(ncclUniqueId), sizeof(ncclUniqueId));
+  job->nranks = nranks;
+  job->rank = rank;
+  PSG_HIP(hipGetDevice(&job->device));
+  const double timeout_s = comm_timeout_s();
+  std::thread(comm_init_thread, job).detach();
+  {
+    std::unique_lock<std::mutex> lk(job->mu);
+    const bool done = job->cv.wait_for(lk, std::chrono::microseconds((int64_t)(timeout_s * 1e6)), [&] { return job->done; });
+    PSG_REQUIRE(done, PSG_ERR_COMM,
+                "psg_comm_init: the RCCL rendezvous of %d ranks (this is rank %d) did not complete within %.0f s "
+                "(PSG_COMM_TIMEOUT_S): a rank did not join",
+                nranks, rank, timeout_s);
+  }
+  if (job->e != hipSuccess) return hip_fail(job->e, "psg_comm_init: hipSetDevice", __FILE__, __LINE__);
+  if (job->r != ncclSuccess) return nccl_fail(job->r, "ncclCommInitRank");
   psg_comm* c = new psg_comm();
   c->rank = rank;
   c->nranks = nranks;
   const char* f = getenv("PSG_COMM_FORCE_COLLECTIVE");
   c->force = f && atoi(f) != 0;
-  (void)hipGetDevice(&c->device);
-  for (int k = 0; k < 2; ++k) {
-    ncclUniqueId id;
-    memcpy(&id, (const char*)id_host + k * sizeof(id), sizeof(id));
-    ncclResult_t r = ncclCommInitRank(&c->comm[k], nranks, id, rank);
-    if (r != ncclSuccess) {
-      if (k == 1) ncclCommDestroy(c->comm[0]);
-      delete c;
-      return nccl_fail(r, "ncclCommInitRank");
-    }
-  }
+  c->device = job->device;
+  for (int k = 0; k < kCommIds; ++k) c->comm[k] = job->comm[k];
   hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -220,11 +292,9 @@ int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* ou
   PSG_REQUIRE(nccl_type(shard->dtype, &t), PSG_ERR_UNSUPPORTED, "psg_comm_push_pull: dtype %d",
               shard->dtype);
   const int es = shard->esize;
-  // bucket b covers [b*chunk, min((b+1)*chunk, blk)) of every rank's block;
-  // chunks are multiples of 64 elements so vector kernels stay aligned
-  uint64_t chunk = (blk + (uint64_t)nbuckets - 1) / (uint64_t)nbuckets;
-  chunk = (chunk + 63) / 64 * 64;
-  const int nb = (int)((blk + chunk - 1) / chunk);
+  std::vector<uint64_t> boff((size_t)nbuckets), bcnt((size_t)nbuckets);
+  int nb = 0;
+  PSG_TRY(psg_comm_bucket_plan(blk, nbuckets, boff.data(), bcnt.data(), nbuckets, &nb));
   PSG_TRY(ensure_scratch(c, blk * es));
   while ((int)c->ev.size() < nb) {
     hipEvent_t e;
@@ -240,8 +310,7 @@ int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* ou
   char* sv = (char*)shard->vals;
   char* sc = (char*)c->scratch;
   for (int b = 0; b < nb; ++b) {
-    const uint64_t off = (uint64_t)b * chunk;
-    const uint64_t cnt = off + chunk <= blk ? chunk : blk - off;
+    const uint64_t off = boff[b], cnt = bcnt[b];
     // Push of bucket b: every rank's chunk b reduced to its owner, then accumulated
     PSG_NCCL(ncclGroupStart());
     for (int r = 0; r < c->nranks; ++r) {
@@ -265,24 +334,47 @@ int psg_comm_push_pull(psg_comm* c, psg_store* shard, const void* vals, void* ou
   return PSG_OK;
 }
 
+int psg_comm_bucket_plan(uint64_t blk, int nbuckets, uint64_t* offs, uint64_t* cnts, int cap, int* nb_out) {
+  PSG_REQUIRE(offs && cnts && nb_out && nbuckets >= 1, PSG_ERR_INVALID, "psg_comm_bucket_plan: bad arguments");
+  *nb_out = 0;
+  if (blk == 0) return PSG_OK;
+  // bucket b covers [b*chunk, min((b+1)*chunk, blk)) of every rank's block;
+  // chunks are multiples of 64 elements so vector kernels stay aligned
+  uint64_t chunk = (blk + (uint64_t)nbuckets - 1) / (uint64_t)nbuckets;
+  chunk = (chunk + 63) / 64 * 64;
+  const int nb = (int)((blk + chunk - 1) / chunk);
+  PSG_REQUIRE(nb <= cap, PSG_ERR_INVALID, "psg_comm_bucket_plan: %d buckets, room for %d", nb, cap);
+  for (int b = 0; b < nb; ++b) {
+    offs[b] = (uint64_t)b * chunk;
+    cnts[b] = offs[b] + chunk <= blk ? chunk : blk - offs[b];
+  }
+  *nb_out = nb;
+  return PSG_OK;
+}
+
 // ---- keyed BSP (configs[3], LR_ps): every rank pushes values for the SAME
 // sorted key array, cut by psg_slice into per-server segments key_pos[r] ..
 // key_pos[r+1].  Push: segment r of every rank is reduced to rank r, which
 // applies it to its store with the keyed handle; Pull: every owner reads its
 // segment and broadcasts it into place.
-static int keyed_args(psg_comm* c, psg_store* s, const uint64_t* keys, uint64_t n,
-                      const uint64_t* kp, uint64_t* maxseg) {
-  PSG_REQUIRE(c && s && kp, PSG_ERR_INVALID, "psg_comm keyed: null argument");
-  PSG_REQUIRE(n == 0 || keys, PSG_ERR_INVALID, "psg_comm keyed: null keys");
-  PSG_REQUIRE(kp[0] == 0 && kp[c->nranks] == n, PSG_ERR_INVALID,
+int psg_comm_keyed_plan(const uint64_t* kp, int nranks, uint64_t n, uint64_t* maxseg) {
+  PSG_REQUIRE(kp && maxseg && nranks >= 1, PSG_ERR_INVALID, "psg_comm keyed: null argument");
+  PSG_REQUIRE(kp[0] == 0 && kp[nranks] == n, PSG_ERR_INVALID,
               "psg_comm keyed: key_pos must cover [0, n) (%llu..%llu vs %llu)",
-              (unsigned long long)kp[0], (unsigned long long)kp[c->nranks], (unsigned long long)n);
+              (unsigned long long)kp[0], (unsigned long long)kp[nranks], (unsigned long long)n);
   *maxseg = 0;
-  for (int r = 0; r < c->nranks; ++r) {
+  for (int r = 0; r < nranks; ++r) {
     PSG_REQUIRE(kp[r] <= kp[r + 1], PSG_ERR_INVALID, "psg_comm keyed: key_pos not ascending");
     if (kp[r + 1] - kp[r] > *maxseg) *maxseg = kp[r + 1] - kp[r];
   }
   return PSG_OK;
+}
+
+static int keyed_args(psg_comm* c, psg_store* s, const uint64_t* keys, uint64_t n,
+                      const uint64_t* kp, uint64_t* maxseg) {
+  PSG_REQUIRE(c && s && kp, PSG_ERR_INVALID, "psg_comm keyed: null argument");
+  PSG_REQUIRE(n == 0 || keys, PSG_ERR_INVALID, "psg_comm keyed: null keys");
+  return psg_comm_keyed_plan(kp, c->nranks, n, maxseg);
 }
 
 int psg_comm_push_keyed(psg_comm* c, psg_store* shard, const uint64_t* keys, const void* vals,

@@ -11,6 +11,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <deque>
 #include <string>
 
 #include "../../include/psg.h"
@@ -134,6 +135,23 @@ inline size_t ipc_alloc_bytes(size_t bytes) {
 // ---- store ------------------------------------------------------------------
 }  // namespace psg
 
+namespace psg {
+// A fused keyed request launched and not yet reaped (psg_store_handle_async).
+struct InflightReq {
+  uint64_t ticket;
+  int op;
+  const uint64_t* q;
+  uint64_t n;
+  const void* vals;
+  void* out;
+  uint32_t ring;  // its completion word: ring_host[ring]
+  uint32_t tag;   // the 24-bit tag that word will carry
+  int wc;         // window-cache entry it ran on
+  hipStream_t stream;
+};
+constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
+}  // namespace psg
+
 struct psg_store {
   int kind;
   int dtype;
@@ -151,19 +169,33 @@ struct psg_store {
   uint64_t slots_cap;
   int* flags;        // device view of flags_host: the kernels raise flags there
   int* flags_host;   // pinned host int[4]: any key absent / out of range / unsorted
-  // Device word the validation pass sets to the request's sequence number when
-  // the request is invalid (unsorted, duplicate or out-of-range keys); every
-  // store-writing kernel of that request reads it first and writes nothing.
+  // Device words (psg_store.hip, kRej* / kPending): the validation pass sets
+  // [0] / [1] to the request's sequence number when a key is out of range /
+  // out of order (every store-writing kernel of that request reads them first
+  // and writes nothing); [2] != 0 gates every later fused request until the
+  // host has done an earlier request's follow-up (insert, out-of-order path).
   int* reject_dev;
   int seq;           // request sequence number (never 0 after the first request)
-  uint32_t done_seq; // completion words the stream or a kernel has been asked to write
-  // k_resolve_apply signals its own completion: every block counts itself in
-  // on one of 8 shard counters, each shard's last block on a top counter, and
-  // the block that completes the top writes the completion word
-  // (psg_store.hip, block_arrive / request_done).  Counters are monotonic;
-  // ctr_base holds each one's value before the next launch.
-  uint32_t* done_ctr;
-  uint32_t ctr_base[9];
+  uint32_t done_seq; // completion words the stream has been asked to write (read_flags)
+  // k_resolve_apply's arrival counters, one set per ring slot: 8 shard
+  // counters and a top counter, 64-bit, each on its own 256 B; zeroed by the
+  // block that completes the request
+  uint64_t* done_ctr;
+  // completion words of the fused requests: tag << 8 | flags, written by the
+  // kernel with one system-scope store (pinned host memory, kRing words)
+  uint32_t* ring_host;
+  uint32_t* ring_dev;
+  uint32_t ring_next;
+  uint32_t tag;
+  // fused requests in flight, in launch (= stream) order
+  std::deque<psg::InflightReq> inflight;
+  uint64_t next_ticket;
+  // the first failure of an asynchronous request not yet reported by psg_store_wait
+  int async_rc;
+  std::string async_msg;
+  // scratch of the out-of-order path (psg_store.hip, general_request)
+  void* gbuf;
+  uint64_t gbuf_bytes;
   // K's generation: bumped whenever the sorted key array changes (insert,
   // clear), so a cached window of an older K is never trusted.
   uint32_t gen;
@@ -207,4 +239,14 @@ int dense_request(int dtype, int op, void* store_vals, const void* vals, void* o
 // Slot-indexed request (gather/scatter).  psg_dense.hip.
 int slot_request(int dtype, int op, void* store_vals, const uint32_t* slots,
                  const void* vals, void* out, uint64_t n, hipStream_t stream);
+// Stable LSD radix sort on bits [0, bits) of keys[n], carrying u32 values
+// (iota: the values are the positions 0..n-1 and vals is not read).  Ping-pongs
+// between (keys, vals) and (keys_alt, vals_alt); *result = 0 or 1 names the
+// pair holding the sorted output.  counts: radix_counts_elems(n) u32 of
+// scratch.  psg_sort.hip.
+uint64_t radix_counts_elems(uint64_t n);
+int radix_sort_u32(uint32_t* keys, uint32_t* vals, uint64_t n, int bits, bool iota, uint32_t* keys_alt,
+                   uint32_t* vals_alt, uint32_t* counts, hipStream_t st, int* result);
+int radix_sort_u64(uint64_t* keys, uint32_t* vals, uint64_t n, int bits, bool iota, uint64_t* keys_alt,
+                   uint32_t* vals_alt, uint32_t* counts, hipStream_t st, int* result);
 }  // namespace psg

@@ -47,12 +47,12 @@ namespace psg {
 constexpr int kTile = 1024;  // request keys per block tile (4 per lane)
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
-// Request flags live in pinned host memory that the kernels write directly
-// (one store of 1 per wave that saw the condition — idempotent, no atomics),
-// so a request needs no flag reset launch and no flag copy: the host zeroes
-// them before the launch and reads them once the request's completion word
-// has appeared (written by the stream, read_flags, or by k_resolve_apply
-// itself, request_done).
+// Request flags of the launches that report through the stream (the
+// two-pass resolve, the DENSE-keyed check, psg_store_resolve): pinned host ints
+// the kernels set (one store of 1 per wave that saw the condition —
+// idempotent, no atomics), zeroed by the host before the launch and read once
+// a stream-written completion word has appeared (read_flags): the end of the
+// kernel orders its stores before that word.
 // F_WINMISS: a cached window did not match its tile (searched inline).
 enum { F_MISSING = 0, F_WINMISS = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
 // the host-memory completion word after the flags; never zeroed by reset_flags
@@ -62,6 +62,18 @@ __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
   if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
 }
 
+// The fused keyed request (k_resolve_apply) reports through ONE word of the
+// store's ring in pinned host memory: bits [8, 32) the request's 24-bit tag,
+// bits [0, 8) its flags:
+enum { W_MISSING = 1, W_WINMISS = 2, W_RANGE = 4, W_UNSORTED = 8, W_GATED = 16 };
+// Device words (reject_dev): the validation pass writes a request's sequence
+// number into [kRejRange] / [kRejUnsorted] when a key is out of the shard's
+// range / out of order.  [kPending] != 0: an earlier request needs the host
+// first (absent keys to insert, or keys out of order to take the
+// order-preserving path); every later fused request then writes nothing and
+// reports W_GATED, and the host replays it after that follow-up.
+constexpr int kRejRange = 0, kRejUnsorted = 1, kPending = 2;
+
 // The store-key window of one request tile: [lo, hi) of K brackets every key
 // between the tile's first and last key (lo = lower_bound(K, first), hi =
 // lower_bound(K, last) + 1, clipped to S).  Valid while K is unchanged (gen).
@@ -70,58 +82,86 @@ struct Win {
   uint32_t lo, hi, gen, pad;
 };
 
-// Completion of a request, signalled by its last kernel (k_resolve_apply)
-// instead of a stream-written word, which costs a separate blit launch (~8.6
-// us per request on MI355X).  Each block, once it knows every host flag it
-// will raise (after the resolve of its last tile), raises them, makes them
-// visible at system scope (raise_flag_sys), and counts itself in with a returning
-// atomic on one of 8 shard counters (blockIdx mod 8, each on its own lines,
-// so 2048 arrivals do not queue on one address); its apply stores go out
-// while that round trip is in flight.  The last block of a shard counts the
-// shard in on the top counter, and the block that completes the top writes
-// the host-mapped completion word.  Counters are monotonic: the host passes
-// the value each one's last add returns (Arrival).  Stores to the store and
-// the reply need no ordering here: only later launches on the same stream
-// read them.  (A posted per-block word in host memory instead — no atomic —
-// took 50-90 us to land for 2048 blocks: PCIe writes serialise.)
+// Completion of a fused request and its flags, ordered by atomicity alone.
+// Every block adds ONE 64-bit value to one of 8 shard counters (blockIdx mod
+// 8, each on its own 256 B, so 2048 arrivals do not queue on one address): 1
+// in bits [0, 12), plus 1 in the field of each condition it saw — absent keys
+// [12, 24), a stale window [24, 36), and for a Pull, which checks its own
+// keys, a key out of range [36, 48) or out of order [48, 60).  The block whose
+// add completes its shard (the value the add returned says so) adds its
+// shard's conditions, as one more such value, to the top counter; the block
+// that completes the top writes the completion word — tag and flags in ONE
+// system-scope store — and zeroes the counters (every block of the launch has
+// arrived: no add can follow).  Each request of the ring has its own counter
+// set, used again kRing requests later.  A read-modify-write
+// returns the latest value of its counter, so the completing sum holds every
+// block's conditions and the word is right by atomicity: no fence, and the
+// host reads nothing but that word.  The apply stores need no ordering here:
+// only later launches on the same stream read them.  (A posted per-block word
+// in host memory instead — no atomic — took 50-90 us to land for 2048 blocks:
+// PCIe writes serialise.)
 constexpr int kArriveShards = 8;
-constexpr int kArriveStride = 64;  // words between counters (256 B)
+constexpr int kArriveStride = 32;  // 64-bit words between counters (256 B)
+constexpr int kField = 12;
+constexpr uint64_t kFieldMask = (1ull << kField) - 1;
 struct Arrival {
-  uint32_t* ctr;  // kArriveShards shard counters, then the top counter
-  uint32_t last[kArriveShards];
-  uint32_t top_last;
+  uint64_t* ctr;                 // kArriveShards shard counters, then the top counter
+  uint32_t cnt[kArriveShards];   // blocks that arrive on each shard
+  uint32_t nsh;                  // shards that receive any block
 };
-// A flag raised on the way to an arrival: a system-scope (write-through)
-// store, drained (vmcnt) before the block's barrier and so before its
-// arrival is counted — no fence, which would write back the XCD's L2.
-__device__ __forceinline__ void raise_flag_sys(int* flags, int which, bool cond) {
-  if (__ballot(cond) && (threadIdx.x & 63) == 0)
-    __hip_atomic_store(flags + which, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// cond bits: 1 absent key, 2 stale window, 4 out of range, 8 out of order
+__device__ __forceinline__ uint64_t arrival_value(uint32_t cond) {
+  uint64_t a = 1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (cond & (1u << k)) a += 1ull << ((k + 1) * kField);
+  return a;
 }
-__device__ __forceinline__ uint32_t block_arrive(int* flags, int missing, int winmiss, int range, int unsorted,
-                                                 const Arrival& a) {
-  raise_flag_sys(flags, F_MISSING, missing != 0);
-  raise_flag_sys(flags, F_WINMISS, winmiss != 0);
-  raise_flag_sys(flags, F_RANGE, range != 0);
-  raise_flag_sys(flags, F_UNSORTED, unsorted != 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+__device__ __forceinline__ uint32_t sum_conditions(uint64_t sum) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if ((sum >> ((k + 1) * kField)) & kFieldMask) c |= 1u << k;
+  return c;
+}
+// Block arrival once every condition of the block is known (after the resolve
+// of its last tile): the block's threads OR theirs into an LDS word (zeroed at
+// kernel start, before a barrier), and thread 0 adds the block's value to its
+// shard.  Returns the shard's count after this add (thread 0).
+__device__ __forceinline__ uint64_t block_arrive(uint32_t cond, uint32_t* s_cond, const Arrival& a) {
+  if (cond) atomicOr(s_cond, cond);
   __syncthreads();
-  uint32_t old = 0;
-  if (threadIdx.x == 0)
-    old = __hip_atomic_fetch_add(a.ctr + (blockIdx.x % kArriveShards) * kArriveStride, 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-  return old;
-}
-__device__ __forceinline__ void request_done(uint32_t ticket, const Arrival& a, uint32_t* word, uint32_t val) {
-  if (threadIdx.x == 0 && ticket == a.last[blockIdx.x % kArriveShards]) {
-    const uint32_t top = __hip_atomic_fetch_add(a.ctr + kArriveShards * kArriveStride, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    // no fence before the word: every block's flags were made visible before
-    // its arrival was counted (raise_flag_sys), and the host reads nothing else
-    // (a system-scope fence here wrote back the XCD's L2 — every dirty store
-    // line of the apply — before the host could learn of the completion)
-    if (top == a.top_last) __hip_atomic_store(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint64_t after = 0;
+  if (threadIdx.x == 0) {
+    const uint64_t v = arrival_value(*s_cond);
+    after = __hip_atomic_fetch_add(a.ctr + (blockIdx.x % kArriveShards) * kArriveStride, v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) + v;
   }
+  return after;
+}
+// uniform: flags every block knows alike (W_GATED, and a Push's rejection
+// read from the reject words); may_pend: raise kPending when the request needs
+// the host's follow-up (absent keys, or keys out of order, and not rejected).
+__device__ __forceinline__ void request_done(uint64_t after, const Arrival& a, uint32_t uniform, int* pending,
+                                             uint32_t* word, uint32_t tag_bits) {
+  if (threadIdx.x != 0 || (after & kFieldMask) != a.cnt[blockIdx.x % kArriveShards]) return;
+  const uint64_t v = arrival_value(sum_conditions(after));  // the shard's conditions, counted once
+  const uint64_t top =
+      __hip_atomic_fetch_add(a.ctr + kArriveShards * kArriveStride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + v;
+  if ((top & kFieldMask) != a.nsh) return;
+  const uint32_t c = sum_conditions(top);
+  uint32_t f = uniform;
+  if (c & 1u) f |= W_MISSING;
+  if (c & 2u) f |= W_WINMISS;
+  if (c & 4u) f |= W_RANGE;
+  if (c & 8u) f |= W_UNSORTED;
+  // zeroed by read-modify-writes, like the adds (one point of coherence for
+  // all of a counter's accesses); the set is next used kRing requests later
+  for (int k = 0; k <= kArriveShards; ++k)
+    (void)__hip_atomic_exchange(a.ctr + k * kArriveStride, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!(f & (W_GATED | W_RANGE)) && (f & (W_MISSING | W_UNSORTED)))
+    __hip_atomic_store(pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(word, tag_bits | f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__ a, uint64_t lo,
@@ -282,17 +322,16 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 // Either kind may be absent (nsearch = 0: the windows cached for this key
 // array are trusted; no stream blocks: a Pull, which checks its own keys).
 // The search blocks come first in dispatch order, so their latency runs under
-// the key stream.  An invalid request sets *reject = seq, which
-// k_resolve_apply checks before it writes anything, and raises F_UNSORTED /
-// F_RANGE for the host.  Bytes: the request keys once (8 B / key, default
+// the key stream.  An invalid request writes seq into reject[kRejRange] /
+// [kRejUnsorted], which k_resolve_apply checks before it writes anything and
+// reports in the request's completion word.  Bytes: the request keys once (8 B / key, default
 // cache policy so k_resolve_apply's re-read right after can hit the Infinity
 // Cache) plus the probes.
 __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __restrict__ q, uint64_t n,
                                                           const uint64_t* __restrict__ K, uint64_t S,
                                                           Win* __restrict__ win, uint32_t gen, uint64_t tileN,
                                                           unsigned nsearch, uint64_t kb, uint64_t ke,
-                                                          int* __restrict__ reject, int seq,
-                                                          int* __restrict__ flags, int vec) {
+                                                          int* __restrict__ reject, int seq, int vec) {
   const uint64_t ntiles = (n + tileN - 1) / tileN;
   if (blockIdx.x < nsearch) {
     const uint64_t waves = (uint64_t)nsearch * (kBlock / 64);
@@ -359,9 +398,8 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
       }
     }
   }
-  if (__ballot(range || unsorted) && (threadIdx.x & 63) == 0) *reject = seq;
-  raise_flag(flags, F_RANGE, range != 0);
-  raise_flag(flags, F_UNSORTED, unsorted != 0);
+  if (__ballot(range) && (threadIdx.x & 63) == 0) reject[kRejRange] = seq;
+  if (__ballot(unsorted) && (threadIdx.x & 63) == 0) reject[kRejUnsorted] = seq;
 }
 
 // DENSE store addressed by explicit keys: the same request validation (keys
@@ -376,7 +414,8 @@ __global__ __launch_bounds__(256) void k_validate_keys(const uint64_t* __restric
     if (i > 0 && q[i - 1] >= key) unsorted = 1;
     if (key < kb || key - kb >= cap) range = 1;
   }
-  if (__ballot(range || unsorted) && (threadIdx.x & 63) == 0) *reject = seq;
+  if (__ballot(range) && (threadIdx.x & 63) == 0) reject[kRejRange] = seq;
+  if (__ballot(unsorted) && (threadIdx.x & 63) == 0) reject[kRejUnsorted] = seq;
   raise_flag(flags, F_RANGE, range != 0);
   raise_flag(flags, F_UNSORTED, unsorted != 0);
 }
@@ -416,27 +455,34 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
                                                        typename Elem<DT>::T* __restrict__ V,
                                                        const typename Elem<DT>::T* __restrict__ vals,
                                                        typename Elem<DT>::T* __restrict__ outv,
-                                                       const int* __restrict__ reject, int seq,
-                                                       int* __restrict__ flags, int vec,
-                                                       Arrival arrival, uint32_t* __restrict__ done_word,
-                                                       uint32_t done_val) {
+                                                       int* __restrict__ rej, int seq, int vec,
+                                                       Arrival arrival, uint32_t* __restrict__ word,
+                                                       uint32_t tag_bits) {
   using E = Elem<DT>;
   using T = typename E::T;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
   constexpr uint32_t winN = 2 * NT * kPerLane;          // LDS window of store keys
   __shared__ uint64_t sK[winN];
   __shared__ uint64_t sBound[2];
+  __shared__ uint32_t s_cond;
   // A request that writes the store was validated as a whole first: if
   // k_validate_windows rejected it, write nothing (every block skips its
   // tiles, uniformly, before any store access, and still signals).  A Pull
   // writes only its reply, so it checks its keys here, in the same pass
-  // (CHECK), and the host rejects it from the flags before anything else
-  // happens (no insert of absent keys).
+  // (CHECK), and the host rejects it from its word before anything else
+  // happens (no insert of absent keys).  A request behind one that awaits
+  // the host's follow-up (kPending) is gated: it writes nothing either.
   constexpr bool CHECK = OP == PSG_PULL;
-  bool skip = false;
-  if constexpr (!CHECK) skip = *reject == seq;
+  if (threadIdx.x == 0) s_cond = 0;
+  __syncthreads();
+  uint32_t uniform = rej[kPending] != 0 ? (uint32_t)W_GATED : 0u;
+  if constexpr (!CHECK) {
+    if (rej[kRejRange] == seq) uniform |= W_RANGE;
+    if (rej[kRejUnsorted] == seq) uniform |= W_UNSORTED;
+  }
+  const bool skip = uniform != 0;
   int missing = 0, range = 0, unsorted = 0, winmiss = 0;
-  uint32_t ticket = 0;
+  uint64_t after = 0;
   bool arrived = false;
   const uint64_t ntiles = skip ? 0 : (n + tileN - 1) / tileN;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -573,7 +619,8 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
       if (!found) missing++;
     }
     if (tile + gridDim.x >= ntiles) {  // this block's last tile (uniform)
-      ticket = block_arrive(flags, missing, winmiss, range, unsorted, arrival);
+      after = block_arrive((missing ? 1u : 0u) | (winmiss ? 2u : 0u) | (range ? 4u : 0u) | (unsorted ? 8u : 0u),
+                           &s_cond, arrival);
       arrived = true;
     }
     // apply.  A lane whose 4 keys are 4 consecutive, 16-B aligned store
@@ -628,8 +675,8 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
     }
     __syncthreads();
   }
-  if (!arrived) ticket = block_arrive(flags, missing, winmiss, range, unsorted, arrival);  // no tile (rejected)
-  request_done(ticket, arrival, done_word, done_val);
+  if (!arrived) after = block_arrive(0u, &s_cond, arrival);  // no tile (rejected, gated, or a spare block)
+  request_done(after, arrival, uniform, rej + kPending, word, tag_bits);
 }
 
 // Block-wide exclusive scan helper over 256 lanes (wave = 64).
@@ -751,7 +798,7 @@ __global__ __launch_bounds__(256) void k_dense_keyed(typename Elem<DT>::T* __res
                                                      uint64_t n, const int* __restrict__ reject,
                                                      int seq) {
   using E = Elem<DT>;
-  if (*reject == seq) return;  // k_validate_keys rejected the request
+  if (reject[kRejRange] == seq || reject[kRejUnsorted] == seq) return;  // rejected by k_validate_keys
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * kBlock) {
     const uint64_t p = keys[i] - kb;
@@ -1022,9 +1069,231 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
   return e;
 }
 
+// ---- the out-of-order path ------------------------------------------------
+// KVServerDefaultHandle walks a request in arrival order (KVApp.h:446-454):
+// `store[key] += vals[i]` per occurrence, and a PushPull answers the running
+// value.  A request whose keys are not strictly ascending — any order, keys
+// repeated — is therefore served by resolving every key (any order), inserting
+// the absent ones, sorting the (slot, position) pairs by slot STABLY (each
+// key's occurrences stay in arrival order; psg_sort.hip), and walking each
+// slot's run in order: one lane per run adds its occurrences one after the
+// other, exactly the reference's sequence of additions, and writes each
+// occurrence's running value to its reply position.
+
+// slots[i] = index of q[i] in K[0..S), or kNoSlot (any order, repeats allowed)
+__global__ __launch_bounds__(256) void k_resolve_any(const uint64_t* __restrict__ q, uint64_t n,
+                                                     const uint64_t* __restrict__ K, uint64_t S,
+                                                     uint32_t* __restrict__ slots) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t key = q[i];
+    const uint64_t p = lower_bound_dev(K, 0, S, key);
+    slots[i] = (p < S && K[p] == key) ? (uint32_t)p : kNoSlot;
+  }
+}
+
+// first occurrences in a sorted array: per-1024-key-tile counts, then compaction
+__global__ __launch_bounds__(256) void k_tile_heads(const uint64_t* __restrict__ a, uint64_t n,
+                                                    uint32_t* __restrict__ counts) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * (kTile / kBlock);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    const uint64_t i = i0 + k;
+    if (i < n && (i == 0 || a[i - 1] != a[i])) c++;
+  }
+  uint32_t tot;
+  block_excl_scan(c, &tot);
+  if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(256) void k_compact_heads(const uint64_t* __restrict__ a, uint64_t n,
+                                                       const uint32_t* __restrict__ offs, uint64_t* __restrict__ out) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * (kTile / kBlock);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    const uint64_t i = i0 + k;
+    if (i < n && (i == 0 || a[i - 1] != a[i])) c++;
+  }
+  uint32_t tot;
+  uint32_t pos = offs[blockIdx.x] + block_excl_scan(c, &tot);
+#pragma unroll
+  for (int k = 0; k < kTile / kBlock; ++k) {
+    const uint64_t i = i0 + k;
+    if (i < n && (i == 0 || a[i - 1] != a[i])) out[pos++] = a[i];
+  }
+}
+
+// One lane per run of equal slots in the slot-sorted pairs (ss, sp): the
+// occurrences in arrival order, each added in turn (Push), each reply the
+// running value (PushPull).
 template <int DT, int OP>
-static int launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals,
-                                void* out, Win* win, uint32_t done_val, hipStream_t st) {
+__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ ss, const uint32_t* __restrict__ sp,
+                                                   uint64_t n, typename Elem<DT>::T* __restrict__ V,
+                                                   const typename Elem<DT>::T* __restrict__ vals,
+                                                   typename Elem<DT>::T* __restrict__ out) {
+  using E = Elem<DT>;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t slot = ss[j];
+    if (j > 0 && ss[j - 1] == slot) continue;  // not the head of its run
+    typename E::T acc = V[slot];
+    uint64_t k = j;
+    do {
+      const uint32_t p = sp[k];
+      acc = E::add1(acc, vals[p]);
+      if constexpr ((OP & PSG_PULL) != 0) out[p] = acc;
+      ++k;
+    } while (k < n && ss[k] == slot);
+    V[slot] = acc;
+  }
+}
+
+// Scratch of the out-of-order path, carved from one growing device block.
+struct GScratch {
+  uint32_t *a, *b, *c, *counts, *tcount;
+  uint64_t *k0, *k1;
+};
+static int general_scratch(psg_store* s, uint64_t n, GScratch* g) {
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  const uint64_t nt = (n + kTile - 1) / kTile + 2;
+  const uint64_t u32n = al(n * 4), u64n = al(n * 8), cnt = al(radix_counts_elems(n) * 4), tc = al(nt * 4);
+  const uint64_t bytes = 3 * u32n + cnt + tc + 2 * u64n;
+  if (s->gbuf_bytes < bytes) {
+    if (s->gbuf) PSG_HIP(hipFree(s->gbuf));
+    s->gbuf = nullptr;
+    s->gbuf_bytes = 0;
+    PSG_HIP(hipMalloc(&s->gbuf, bytes));
+    s->gbuf_bytes = bytes;
+  }
+  char* p = (char*)s->gbuf;
+  g->a = (uint32_t*)p, p += u32n;
+  g->b = (uint32_t*)p, p += u32n;
+  g->c = (uint32_t*)p, p += u32n;
+  g->counts = (uint32_t*)p, p += cnt;
+  g->tcount = (uint32_t*)p, p += tc;
+  g->k0 = (uint64_t*)p, p += u64n;
+  g->k1 = (uint64_t*)p;
+  return PSG_OK;
+}
+
+static int read_count(const uint32_t* dev, uint64_t* out, hipStream_t st) {
+  uint32_t m32 = 0;
+  PSG_HIP(hipMemcpyAsync(&m32, dev, sizeof(m32), hipMemcpyDeviceToHost, st));
+  PSG_HIP(hipStreamSynchronize(st));
+  *out = m32;
+  return PSG_OK;
+}
+
+// The absent keys of q[0..n) (s->slots[i] == kNoSlot; any order, repeats)
+// inserted with value 0 (operator[], KVApp.h:449/452): compacted, sorted,
+// made unique, merged into K.  *inserted = how many.
+static int insert_missing_any(psg_store* s, const uint64_t* q, uint64_t n, const GScratch& g, uint64_t* inserted,
+                              hipStream_t st) {
+  *inserted = 0;
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  k_tile_missing<<<(unsigned)ntiles, kBlock, 0, st>>>(s->slots, n, g.tcount);
+  k_scan_counts<<<1, kBlock, 0, st>>>(g.tcount, ntiles);
+  uint64_t m = 0;
+  PSG_TRY(read_count(g.tcount + ntiles, &m, st));
+  if (m == 0) return PSG_OK;
+  k_compact_missing<<<(unsigned)ntiles, kBlock, 0, st>>>(q, s->slots, n, g.tcount, g.k0);
+  int res = 0;
+  PSG_TRY(radix_sort_u64(g.k0, g.a, m, 64, true, g.k1, g.b, g.counts, st, &res));
+  const uint64_t* sorted = res ? g.k1 : g.k0;
+  uint64_t* uniq = res ? g.k0 : g.k1;
+  const uint64_t mt = (m + kTile - 1) / kTile;
+  k_tile_heads<<<(unsigned)mt, kBlock, 0, st>>>(sorted, m, g.tcount);
+  k_scan_counts<<<1, kBlock, 0, st>>>(g.tcount, mt);
+  uint64_t mu = 0;
+  PSG_TRY(read_count(g.tcount + mt, &mu, st));
+  k_compact_heads<<<(unsigned)mt, kBlock, 0, st>>>(sorted, m, g.tcount, uniq);
+  PSG_HIP(hipGetLastError());
+  switch (s->dtype) {
+    case PSG_F32: PSG_TRY(merge_insert<float>(s, uniq, mu, st)); break;
+    case PSG_F64: PSG_TRY(merge_insert<double>(s, uniq, mu, st)); break;
+    case PSG_F16: PSG_TRY(merge_insert<_Float16>(s, uniq, mu, st)); break;
+    case PSG_BF16: PSG_TRY(merge_insert<__bf16>(s, uniq, mu, st)); break;
+    default: return PSG_ERR_UNSUPPORTED;
+  }
+  *inserted = mu;
+  return PSG_OK;
+}
+
+static int bit_width(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+// A request whose keys are not strictly ascending (already checked to lie in
+// the store's range), served in arrival order.  Synchronous.
+template <int DT>
+static int general_request(psg_store* s, int op, const uint64_t* q, const void* vals, void* out, uint64_t n,
+                           hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  PSG_TRY(ensure_slots(s, n));
+  GScratch g;
+  PSG_TRY(general_scratch(s, n, &g));
+  uint32_t* slots = s->slots;
+  uint64_t slot_space;
+  if (s->kind == PSG_STORE_SORTED) {
+    if (s->size) k_resolve_any<<<grid_n(n, kBlock), kBlock, 0, st>>>(q, n, s->keys, s->size, slots);
+    else PSG_HIP(hipMemsetAsync(slots, 0xff, n * sizeof(uint32_t), st));
+    uint64_t inserted = 0;
+    PSG_TRY(insert_missing_any(s, q, n, g, &inserted, st));
+    if (inserted) k_resolve_any<<<grid_n(n, kBlock), kBlock, 0, st>>>(q, n, s->keys, s->size, slots);
+    slot_space = s->size;
+  } else {
+    reset_flags(s);
+    k_dense_slots<<<grid_n(n, kBlock), kBlock, 0, st>>>(q, n, s->key_begin, s->capacity, slots, s->flags);
+    slot_space = s->capacity;
+  }
+  PSG_HIP(hipGetLastError());
+  if (op == PSG_PULL) {  // reads only: every occurrence gets its key's value
+    PSG_TRY(slot_request(s->dtype, PSG_PULL, s->vals, slots, nullptr, out, n, st));
+  } else {
+    int res = 0;
+    const int bits = std::max(1, bit_width(slot_space ? slot_space - 1 : 0));
+    PSG_TRY(radix_sort_u32(slots, g.a, n, bits, true, g.b, g.c, g.counts, st, &res));
+    const uint32_t* ss = res ? g.b : slots;
+    const uint32_t* sp = res ? g.c : g.a;
+    const unsigned gr = grid_n(n, kBlock);
+    if (op == PSG_PUSH)
+      k_seg_apply<DT, PSG_PUSH><<<gr, kBlock, 0, st>>>(ss, sp, n, (T*)s->vals, (const T*)vals, (T*)out);
+    else
+      k_seg_apply<DT, PSG_PUSH | PSG_PULL><<<gr, kBlock, 0, st>>>(ss, sp, n, (T*)s->vals, (const T*)vals, (T*)out);
+    PSG_HIP(hipGetLastError());
+  }
+  PSG_HIP(hipStreamSynchronize(st));
+  return PSG_OK;
+}
+
+static int general_dispatch(psg_store* s, int op, const uint64_t* q, const void* vals, void* out, uint64_t n,
+                            hipStream_t st) {
+  switch (s->dtype) {
+    case PSG_F32: return general_request<PSG_F32>(s, op, q, vals, out, n, st);
+    case PSG_F64: return general_request<PSG_F64>(s, op, q, vals, out, n, st);
+    case PSG_F16: return general_request<PSG_F16>(s, op, q, vals, out, n, st);
+    default: return general_request<PSG_BF16>(s, op, q, vals, out, n, st);
+  }
+}
+
+// ---- fused requests, in flight -------------------------------------------
+// A new request: its sequence number tags the reject words (never reset: a
+// stale value names an older request).
+static int next_seq(psg_store* s) {
+  s->seq = s->seq == 0x7fffffff ? 1 : s->seq + 1;
+  return s->seq;
+}
+static uint32_t next_tag(psg_store* s) {
+  s->tag = (s->tag + 1) & 0xffffffu;
+  if (s->tag == 0) s->tag = 1;
+  return s->tag;
+}
+
+static int drain(psg_store* s);
+
+// Launch one fused request — k_validate_windows (skipped for a Pull on
+// trusted windows), then k_resolve_apply — and return without waiting.  Its
+// completion word arrives in ring slot rec->ring.
+template <int DT, int OP>
+static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals, void* out, Win* win,
+                         const InflightReq& rec, hipStream_t st) {
   using T = typename Elem<DT>::T;
   const int nt = ra_block();
   const uint64_t ntiles = (n + (uint64_t)nt * kPerLane - 1) / ((uint64_t)nt * kPerLane);
@@ -1033,17 +1302,15 @@ static int launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, con
                   (aligned16(q) ? 2 : 0);
   const unsigned g = grid_n(ntiles, 1);
   Arrival arr;
-  arr.ctr = s->done_ctr;
-  unsigned nsh = 0;
+  arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
+  arr.nsh = 0;
   for (int j = 0; j < kArriveShards; ++j) {
-    const uint32_t cnt = g > (unsigned)j ? (g - 1 - j) / kArriveShards + 1 : 0;
-    arr.last[j] = s->ctr_base[j] + cnt - 1;  // unused when cnt == 0
-    nsh += cnt ? 1 : 0;
+    arr.cnt[j] = g > (unsigned)j ? (g - 1 - j) / kArriveShards + 1 : 0;
+    arr.nsh += arr.cnt[j] ? 1 : 0;
   }
-  arr.top_last = s->ctr_base[kArriveShards] + nsh - 1;
 #define PSG_RA_ARGS                                                                                     \
   q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end, (T*)s->vals, (const T*)vals, (T*)out, \
-      s->reject_dev, s->seq, s->flags, vec, arr, reinterpret_cast<uint32_t*>(s->flags + kDoneWord), done_val
+      s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8
   if (nt == 1024)
     k_resolve_apply<DT, OP, 1024><<<g, 1024, 0, st>>>(PSG_RA_ARGS);
   else if (nt == 512)
@@ -1051,51 +1318,29 @@ static int launch_resolve_apply(psg_store* s, const uint64_t* q, uint64_t n, con
   else
     k_resolve_apply<DT, OP, 256><<<g, 256, 0, st>>>(PSG_RA_ARGS);
 #undef PSG_RA_ARGS
-  PSG_HIP(hipGetLastError());
-  // every block counted itself in on its shard, every non-empty shard on the top
-  for (int j = 0; j < kArriveShards; ++j) s->ctr_base[j] += g > (unsigned)j ? (g - 1 - j) / kArriveShards + 1 : 0;
-  s->ctr_base[kArriveShards] += nsh;
-  return PSG_OK;
 }
 
-// A new request: its sequence number tags the reject word (never reset: a
-// stale value names an older request).
-static int next_seq(psg_store* s) {
-  s->seq = s->seq == 0x7fffffff ? 1 : s->seq + 1;
-  return s->seq;
-}
-
-// Wait for the completion word k_resolve_apply writes (request_done); after
-// 2 ms (a long request, or a fault) fall back to hipStreamSynchronize, which
-// also reports any error.  PSG_SYNC_POLL=0 always synchronises the stream.
-static int wait_done(psg_store* s, uint32_t want, hipStream_t st) {
-  if (sync_poll()) {
-    const volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(s->flags_host + kDoneWord);
-    auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 0;; ++spin) {
-      if (*w == want) {
-        std::atomic_thread_fence(std::memory_order_acquire);
-        return PSG_OK;
-      }
-      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
-      __builtin_ia32_pause();
-    }
-  }
-  PSG_HIP(hipStreamSynchronize(st));
-  return PSG_OK;
-}
-
-// Window-cache policy.  A key array seen before whose windows the previous
-// request confirmed skips the search pre-pass (trusted); the kernel still
-// checks every window and searches a stale one inline (F_WINMISS).  A key
-// array that keeps changing under one pointer (two misses) always gets the
-// pre-pass, so it never pays the slower inline searches twice.
 template <int DT>
-static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals,
-                         void* out, hipStream_t st) {
+static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals, void* out,
+                        hipStream_t st, InflightReq* rec) {
   const int nt = ra_block();
   const uint64_t tile = (uint64_t)nt * kPerLane;
   const uint64_t ntiles = (n + tile - 1) / tile;
+  // the window-cache entry (win_entry's choice): requests in flight may share
+  // one — every kernel checks each window against its own tile's end keys and
+  // K's generation — but growing one frees windows an in-flight kernel may
+  // still read, so that waits for them first
+  if (!s->inflight.empty()) {
+    const psg_store::WinCache* pick = nullptr;
+    for (auto& c : s->wc)
+      if (c.win && c.q == q && c.n == n) pick = &c;
+    if (!pick) {
+      pick = &s->wc[0];
+      for (auto& c : s->wc)
+        if (c.last_use < pick->last_use) pick = &c;
+    }
+    if (pick->cap_tiles < ntiles) PSG_TRY(drain(s));
+  }
   psg_store::WinCache* wc = win_entry(s, q, n, ntiles);
   PSG_REQUIRE(wc, PSG_ERR_HIP, "SORTED store: window cache allocation failed");
   Win* win = static_cast<Win*>(wc->win);
@@ -1104,7 +1349,6 @@ static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, co
     return e ? atoi(e) : 1;
   }();
   const bool trusted = cache_on && wc->trusted != 0 && (uint32_t)wc->trusted == s->gen;
-  reset_flags(s);
   const int seq = next_seq(s);
   // search blocks: one wave per window bound (2 per tile); key-stream blocks:
   // 2048 keys each, capped at the streaming grid.  A Pull checks its keys
@@ -1113,23 +1357,178 @@ static int resolve_apply(psg_store* s, int op, const uint64_t* q, uint64_t n, co
   const unsigned nval = op == PSG_PULL ? 0u : grid_n(n, (uint64_t)kBlock * 8);
   if (nsearch + nval > 0)
     k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
-                                                         s->key_begin, s->key_end, s->reject_dev, seq, s->flags,
+                                                         s->key_begin, s->key_end, s->reject_dev, seq,
                                                          aligned16(q) ? 1 : 0);
-  PSG_HIP(hipGetLastError());
-  const uint32_t want = ++s->done_seq;
+  rec->ticket = ++s->next_ticket;
+  rec->op = op;
+  rec->q = q;
+  rec->n = n;
+  rec->vals = vals;
+  rec->out = out;
+  rec->ring = s->ring_next;
+  s->ring_next = (s->ring_next + 1) % kRing;
+  rec->tag = next_tag(s);
+  rec->wc = (int)(wc - s->wc);
+  rec->stream = st;
   switch (op) {
-    case PSG_PUSH: PSG_TRY((launch_resolve_apply<DT, PSG_PUSH>(s, q, n, vals, out, win, want, st))); break;
-    case PSG_PULL: PSG_TRY((launch_resolve_apply<DT, PSG_PULL>(s, q, n, vals, out, win, want, st))); break;
-    default: PSG_TRY((launch_resolve_apply<DT, PSG_PUSH | PSG_PULL>(s, q, n, vals, out, win, want, st))); break;
+    case PSG_PUSH: launch_apply<DT, PSG_PUSH>(s, q, n, vals, out, win, *rec, st); break;
+    case PSG_PULL: launch_apply<DT, PSG_PULL>(s, q, n, vals, out, win, *rec, st); break;
+    default: launch_apply<DT, PSG_PUSH | PSG_PULL>(s, q, n, vals, out, win, *rec, st); break;
   }
-  PSG_TRY(wait_done(s, want, st));
-  if (s->flags_host[F_WINMISS]) {
-    wc->trusted = 0;
-    wc->strikes++;
-  } else if (wc->strikes < 2 && !s->flags_host[F_UNSORTED] && !s->flags_host[F_RANGE]) {
-    wc->trusted = (int)s->gen;  // trusted while K keeps this generation
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+// Wait for a fused request's completion word; after 2 ms (a long request, or a
+// fault) synchronise the stream, which also reports any error.
+// PSG_SYNC_POLL=0 always synchronises the stream first (A/B).
+static int wait_word(psg_store* s, const InflightReq& r, uint32_t* flags) {
+  const volatile uint32_t* w = s->ring_host + r.ring;
+  bool synced = false;
+  if (!sync_poll()) {
+    PSG_HIP(hipStreamSynchronize(r.stream));
+    synced = true;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    const uint32_t v = *w;
+    if ((v >> 8) == r.tag) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      *flags = v & 0xffu;
+      return PSG_OK;
+    }
+    if (synced) break;
+    if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      PSG_HIP(hipStreamSynchronize(r.stream));
+      synced = true;
+    }
+    __builtin_ia32_pause();
+  }
+  set_error("SORTED store: request %llu finished without its completion word", (unsigned long long)r.ticket);
+  return PSG_ERR_HIP;
+}
+
+// After a fused request's word: the window-cache policy, then what the word
+// asks of the host.  A key outside the shard rejects the request (nothing was
+// written); keys out of order or repeated take the order-preserving path (the
+// fused kernels wrote nothing but, for a Pull, its reply, which that path
+// rewrites); absent keys are inserted and the request applied to them.
+template <int DT>
+static int finish(psg_store* s, const InflightReq& r, uint32_t f) {
+  psg_store::WinCache& wc = s->wc[r.wc];
+  if (wc.q == r.q && wc.n == r.n) {
+    if (f & W_WINMISS) {
+      wc.trusted = 0;
+      wc.strikes++;
+    } else if (wc.strikes < 2 && !(f & (W_RANGE | W_UNSORTED))) {
+      wc.trusted = (int)s->gen;  // trusted while K keeps this generation
+    }
+  }
+  if (f & W_RANGE)
+    PSG_REQUIRE(false, PSG_ERR_RANGE, "request key outside the store range [%llu, %llu) (nothing applied)",
+                (unsigned long long)s->key_begin, (unsigned long long)s->key_end);
+  if (f & W_UNSORTED) return general_request<DT>(s, r.op, r.q, r.vals, r.out, r.n, r.stream);
+  if (!(f & W_MISSING)) return PSG_OK;
+  // the fused pass kept no slots: resolve again (the keys have not changed)
+  // so the insert and the fixup know which keys were absent
+  PSG_TRY(ensure_slots(s, r.n));
+  PSG_TRY(launch_resolve(s, r.q, r.n, s->slots, r.stream));
+  PSG_TRY(insert_missing(s, r.q, r.n, r.stream));
+  PSG_TRY(launch_resolve(s, r.q, r.n, s->slots2, r.stream));
+  PSG_TRY(run_fixup<DT>(s, r.op, r.vals, r.out, r.n, r.stream));
+  PSG_TRY(read_flags(s, r.stream));
+  PSG_REQUIRE(s->flags_host[F_MISSING] == 0, PSG_ERR_HIP, "SORTED store: keys still absent after insert");
+  return PSG_OK;
+}
+
+// The status of a reaped request: returned to its synchronous caller (own),
+// else kept for psg_store_wait (the first failure).
+static void note(psg_store* s, uint64_t ticket, int rc, uint64_t own, int* own_rc) {
+  if (ticket == own) {
+    *own_rc = rc;
+    return;
+  }
+  if (rc != PSG_OK && s->async_rc == PSG_OK) {
+    s->async_rc = rc;
+    s->async_msg = psg_last_error();
+  }
+}
+
+// Reap the fused requests in flight, in launch order, up to ticket `upto`.
+// A request whose word asks for the host's follow-up has raised kPending, so
+// every request launched after it wrote nothing and reports W_GATED: those
+// are waited for, the follow-up runs, kPending is cleared, and the gated
+// requests are replayed in their order, each to completion — the store sees
+// exactly the requests' sequence.
+template <int DT>
+static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
+  auto replay = [&](const InflightReq& g) {
+    InflightReq r2;
+    int rc = launch_fused<DT>(s, g.op, g.q, g.n, g.vals, g.out, g.stream, &r2);
+    if (rc == PSG_OK) {
+      s->inflight.push_back(r2);
+      int rc2 = PSG_OK;
+      rc = reap_t<DT>(s, r2.ticket, r2.ticket, &rc2);
+      if (rc == PSG_OK) rc = rc2;
+    }
+    note(s, g.ticket, rc, own, own_rc);
+  };
+  while (!s->inflight.empty() && s->inflight.front().ticket <= upto) {
+    const InflightReq r = s->inflight.front();
+    s->inflight.pop_front();
+    uint32_t f = 0;
+    int rc = wait_word(s, r, &f);
+    if (rc != PSG_OK) {
+      note(s, r.ticket, rc, own, own_rc);
+      s->inflight.clear();  // a lost word: the stream is broken
+      return rc;
+    }
+    if (f & W_GATED) {  // gated by a follow-up already done (or an earlier failure)
+      PSG_HIP(hipMemsetAsync(s->reject_dev + kPending, 0, sizeof(int), r.stream));
+      replay(r);
+      continue;
+    }
+    const bool follow = !(f & W_RANGE) && (f & (W_MISSING | W_UNSORTED));
+    if (!follow) {
+      note(s, r.ticket, finish<DT>(s, r, f), own, own_rc);
+      continue;
+    }
+    std::vector<std::pair<InflightReq, uint32_t>> later;
+    for (const InflightReq& g : s->inflight) {
+      uint32_t gf = 0;
+      rc = wait_word(s, g, &gf);
+      if (rc != PSG_OK) {
+        note(s, g.ticket, rc, own, own_rc);
+        s->inflight.clear();
+        return rc;
+      }
+      later.emplace_back(g, gf);
+    }
+    s->inflight.clear();
+    note(s, r.ticket, finish<DT>(s, r, f), own, own_rc);
+    PSG_HIP(hipMemsetAsync(s->reject_dev + kPending, 0, sizeof(int), r.stream));
+    for (auto& [g, gf] : later) {
+      if (gf & W_GATED) replay(g);
+      else note(s, g.ticket, finish<DT>(s, g, gf), own, own_rc);  // (cannot happen: kPending was up)
+    }
   }
   return PSG_OK;
+}
+
+static int reap(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
+  switch (s->dtype) {
+    case PSG_F32: return reap_t<PSG_F32>(s, upto, own, own_rc);
+    case PSG_F64: return reap_t<PSG_F64>(s, upto, own, own_rc);
+    case PSG_F16: return reap_t<PSG_F16>(s, upto, own, own_rc);
+    default: return reap_t<PSG_BF16>(s, upto, own, own_rc);
+  }
+}
+
+// Every request in flight complete (their failures kept for psg_store_wait).
+static int drain(psg_store* s) {
+  if (s->inflight.empty()) return PSG_OK;
+  int unused = PSG_OK;
+  return reap(s, ~0ull, 0, &unused);
 }
 
 // PSG_SORTED_FUSED=0: the two-pass form (resolve to slots, then k_slots), for A/B runs.
@@ -1141,33 +1540,29 @@ static bool sorted_fused() {
   return on;
 }
 
-static int sorted_request(psg_store* s, int op, const uint64_t* q, const void* vals, void* out,
-                          uint64_t n, hipStream_t st) {
+static int launch_fused_any(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals, void* out,
+                            hipStream_t st, InflightReq* rec) {
+  switch (s->dtype) {
+    case PSG_F32: return launch_fused<PSG_F32>(s, op, q, n, vals, out, st, rec);
+    case PSG_F64: return launch_fused<PSG_F64>(s, op, q, n, vals, out, st, rec);
+    case PSG_F16: return launch_fused<PSG_F16>(s, op, q, n, vals, out, st, rec);
+    default: return launch_fused<PSG_BF16>(s, op, q, n, vals, out, st, rec);
+  }
+}
+
+// The two-pass form (an empty store, or the A/B switch), synchronous: the
+// flags are read before the slot pass writes anything.
+static int sorted_twopass(psg_store* s, int op, const uint64_t* q, const void* vals, void* out, uint64_t n,
+                          hipStream_t st) {
   PSG_TRY(ensure_slots(s, n));
-  if (sorted_fused() && s->size > 0) {
-    switch (s->dtype) {
-      case PSG_F32: PSG_TRY(resolve_apply<PSG_F32>(s, op, q, n, vals, out, st)); break;
-      case PSG_F64: PSG_TRY(resolve_apply<PSG_F64>(s, op, q, n, vals, out, st)); break;
-      case PSG_F16: PSG_TRY(resolve_apply<PSG_F16>(s, op, q, n, vals, out, st)); break;
-      default: PSG_TRY(resolve_apply<PSG_BF16>(s, op, q, n, vals, out, st)); break;
-    }
-  } else {
-    // two-pass form (an empty store, or the A/B switch): the flags are read
-    // before the slot pass writes anything
-    PSG_TRY(launch_resolve(s, q, n, s->slots, st));
-    PSG_TRY(read_flags(s, st));
-    PSG_TRY(check_request_flags(s));
-    PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
-    PSG_TRY(read_flags(s, st));
-  }
-  // (the fused form has waited for its own completion word)
-  PSG_TRY(check_request_flags(s));  // rejected by k_validate_windows: nothing was written
+  PSG_TRY(launch_resolve(s, q, n, s->slots, st));
+  PSG_TRY(read_flags(s, st));
+  PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE, "request key outside the store range [%llu, %llu)",
+              (unsigned long long)s->key_begin, (unsigned long long)s->key_end);
+  if (s->flags_host[F_UNSORTED]) return general_dispatch(s, op, q, vals, out, n, st);
+  PSG_TRY(slot_request(s->dtype, op, s->vals, s->slots, vals, out, n, st));
+  PSG_TRY(read_flags(s, st));
   if (s->flags_host[F_MISSING] == 0) return PSG_OK;
-  if (sorted_fused() && s->size > 0) {
-    // the fused pass kept no slots: resolve again (the keys have not changed)
-    // so the insert and the fixup know which keys were absent
-    PSG_TRY(launch_resolve(s, q, n, s->slots, st));
-  }
   PSG_TRY(insert_missing(s, q, n, st));
   PSG_TRY(launch_resolve(s, q, n, s->slots2, st));
   switch (s->dtype) {
@@ -1182,6 +1577,8 @@ static int sorted_request(psg_store* s, int op, const uint64_t* q, const void* v
 }
 
 // Resolve q to slots (psg_store_resolve), inserting absent keys when asked.
+// A slot list must name each key once, in ascending order (the cached-slot
+// kernels update each slot from one lane).
 static int sorted_resolve(psg_store* s, const uint64_t* q, uint64_t n, bool insert, hipStream_t st) {
   PSG_TRY(ensure_slots(s, n));
   PSG_TRY(launch_resolve(s, q, n, s->slots, st));
@@ -1220,6 +1617,47 @@ static int run_dense_keyed(psg_store* s, int op, const uint64_t* keys, const voi
   return PSG_OK;
 }
 
+// One request, synchronously: its status is the return value.
+static int handle_sync(psg_store* s, int flags, const uint64_t* keys, uint64_t first_key, const void* vals,
+                       void* out, uint64_t n, hipStream_t st) {
+  PSG_TRY(drain(s));
+  if (s->kind == PSG_STORE_DENSE) {
+    if (!keys) {
+      PSG_REQUIRE(first_key >= s->key_begin && first_key - s->key_begin <= s->capacity &&
+                      n <= s->capacity - (first_key - s->key_begin),
+                  PSG_ERR_RANGE, "dense request [%llu, +%llu) outside store slots [%llu, +%llu)",
+                  (unsigned long long)first_key, (unsigned long long)n,
+                  (unsigned long long)s->key_begin, (unsigned long long)s->capacity);
+      char* base = (char*)s->vals + (first_key - s->key_begin) * s->esize;
+      return dense_request(s->dtype, flags, base, vals, out, n, st);
+    }
+    reset_flags(s);
+    int rc;
+    switch (s->dtype) {
+      case PSG_F32: rc = run_dense_keyed<PSG_F32>(s, flags, keys, vals, out, n, st); break;
+      case PSG_F64: rc = run_dense_keyed<PSG_F64>(s, flags, keys, vals, out, n, st); break;
+      case PSG_F16: rc = run_dense_keyed<PSG_F16>(s, flags, keys, vals, out, n, st); break;
+      default: rc = run_dense_keyed<PSG_BF16>(s, flags, keys, vals, out, n, st); break;
+    }
+    PSG_TRY(rc);
+    PSG_TRY(read_flags(s, st));
+    PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE,
+                "request key outside the DENSE store slots [%llu, +%llu) (nothing applied)",
+                (unsigned long long)s->key_begin, (unsigned long long)s->capacity);
+    // keys out of order or repeated: applied in arrival order (KVApp.h:446-454)
+    if (s->flags_host[F_UNSORTED]) return general_dispatch(s, flags, keys, vals, out, n, st);
+    return PSG_OK;
+  }
+  PSG_REQUIRE(keys, PSG_ERR_INVALID, "SORTED store needs explicit keys");
+  if (!sorted_fused() || s->size == 0) return sorted_twopass(s, flags, keys, vals, out, n, st);
+  InflightReq rec;
+  PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec));
+  s->inflight.push_back(rec);
+  int own_rc = PSG_OK;
+  PSG_TRY(reap(s, rec.ticket, rec.ticket, &own_rc));
+  return own_rc;
+}
+
 }  // namespace psg
 
 using namespace psg;
@@ -1239,8 +1677,7 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
     PSG_REQUIRE(capacity > 0 && capacity <= key_end - key_begin, PSG_ERR_INVALID,
                 "psg_store_create: DENSE capacity %llu does not fit the key range",
                 (unsigned long long)capacity);
-  psg_store* s = new psg_store();
-  memset(s, 0, sizeof(*s));
+  psg_store* s = new psg_store();  // value-initialised: every plain field zero
   s->kind = kind;
   s->dtype = dtype;
   s->esize = es;
@@ -1258,10 +1695,16 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
   if ((e = hipHostGetDevicePointer((void**)&s->flags, s->flags_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(flags)", __FILE__, __LINE__));
   memset(s->flags_host, 0, (F_NFLAGS + 1) * sizeof(int));
+  if ((e = hipHostMalloc((void**)&s->ring_host, kRing * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+      hipSuccess)
+    return fail(hip_fail(e, "hipHostMalloc(completion ring)", __FILE__, __LINE__));
+  if ((e = hipHostGetDevicePointer((void**)&s->ring_dev, s->ring_host, 0)) != hipSuccess)
+    return fail(hip_fail(e, "hipHostGetDevicePointer(completion ring)", __FILE__, __LINE__));
+  memset(s->ring_host, 0, kRing * sizeof(uint32_t));
   if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
       (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
-    return fail(hip_fail(e, "hipMalloc(reject word)", __FILE__, __LINE__));
-  constexpr size_t kCtrBytes = (kArriveShards + 1) * kArriveStride * sizeof(uint32_t);
+    return fail(hip_fail(e, "hipMalloc(reject words)", __FILE__, __LINE__));
+  constexpr size_t kCtrBytes = (size_t)kRing * (kArriveShards + 1) * kArriveStride * sizeof(uint64_t);
   if ((e = hipMalloc((void**)&s->done_ctr, kCtrBytes)) != hipSuccess ||
       (e = hipMemset(s->done_ctr, 0, kCtrBytes)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(completion counters)", __FILE__, __LINE__));
@@ -1292,12 +1735,15 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
 
 int psg_store_destroy(psg_store* s) {
   if (!s) return PSG_OK;
+  (void)drain(s);
   if (s->vals) (void)hipFree(s->vals);
   if (s->keys) (void)hipFree(s->keys);
   if (s->slots) (void)hipFree(s->slots);
   if (s->slots2) (void)hipFree(s->slots2);
   if (s->wlo) (void)hipFree(s->wlo);
+  if (s->gbuf) (void)hipFree(s->gbuf);
   if (s->flags_host) (void)hipHostFree(s->flags_host);
+  if (s->ring_host) (void)hipHostFree(s->ring_host);
   if (s->reject_dev) (void)hipFree(s->reject_dev);
   if (s->done_ctr) (void)hipFree(s->done_ctr);
   for (auto& c : s->wc)
@@ -1308,6 +1754,7 @@ int psg_store_destroy(psg_store* s) {
 
 int psg_store_get_info(psg_store* s, psg_store_info* info) {
   PSG_REQUIRE(s && info, PSG_ERR_INVALID, "psg_store_get_info: null argument");
+  PSG_TRY(drain(s));  // a request in flight may still insert keys
   info->kind = s->kind;
   info->dtype = s->dtype;
   info->key_begin = s->key_begin;
@@ -1321,6 +1768,7 @@ int psg_store_get_info(psg_store* s, psg_store_info* info) {
 
 int psg_store_clear(psg_store* s, psg_stream stream) {
   PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_clear: null store");
+  PSG_TRY(drain(s));
   if (s->kind == PSG_STORE_DENSE) {
     PSG_HIP(hipMemsetAsync(s->vals, 0, s->capacity * s->esize, (hipStream_t)stream));
   } else {
@@ -1330,44 +1778,58 @@ int psg_store_clear(psg_store* s, psg_stream stream) {
   return PSG_OK;
 }
 
+static int handle_args(psg_store* s, int flags, const void* vals, void* out) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_handle: null store");
+  PSG_REQUIRE(flags >= 1 && flags <= 3, PSG_ERR_INVALID, "psg_store_handle: bad flags %d", flags);
+  PSG_REQUIRE(!(flags & PSG_PUSH) || vals, PSG_ERR_INVALID, "push without vals");
+  PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
+  return PSG_OK;
+}
+
 int psg_store_handle(psg_store* s, int flags, const uint64_t* keys, uint64_t first_key,
                      const void* vals, void* out, uint64_t n, psg_stream stream) {
   PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_handle: null store");
   PSG_REQUIRE(flags >= 1 && flags <= 3, PSG_ERR_INVALID, "psg_store_handle: bad flags %d", flags);
   if (n == 0) return PSG_OK;
-  PSG_REQUIRE(!(flags & PSG_PUSH) || vals, PSG_ERR_INVALID, "push without vals");
-  PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
+  PSG_TRY(handle_args(s, flags, vals, out));
+  return handle_sync(s, flags, keys, first_key, vals, out, n, (hipStream_t)stream);
+}
+
+int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys, uint64_t first_key, const void* vals,
+                           void* out, uint64_t n, psg_stream stream, uint64_t* ticket) {
+  PSG_REQUIRE(s && ticket, PSG_ERR_INVALID, "psg_store_handle_async: null argument");
+  *ticket = 0;
+  PSG_REQUIRE(flags >= 1 && flags <= 3, PSG_ERR_INVALID, "psg_store_handle_async: bad flags %d", flags);
+  if (n == 0) return PSG_OK;
+  PSG_TRY(handle_args(s, flags, vals, out));
   hipStream_t st = (hipStream_t)stream;
-  if (s->kind == PSG_STORE_DENSE) {
-    if (!keys) {
-      PSG_REQUIRE(first_key >= s->key_begin && first_key - s->key_begin <= s->capacity &&
-                      n <= s->capacity - (first_key - s->key_begin),
-                  PSG_ERR_RANGE, "dense request [%llu, +%llu) outside store slots [%llu, +%llu)",
-                  (unsigned long long)first_key, (unsigned long long)n,
-                  (unsigned long long)s->key_begin, (unsigned long long)s->capacity);
-      char* base = (char*)s->vals + (first_key - s->key_begin) * s->esize;
-      return dense_request(s->dtype, flags, base, vals, out, n, st);
-    }
-    reset_flags(s);
-    int rc;
-    switch (s->dtype) {
-      case PSG_F32: rc = run_dense_keyed<PSG_F32>(s, flags, keys, vals, out, n, st); break;
-      case PSG_F64: rc = run_dense_keyed<PSG_F64>(s, flags, keys, vals, out, n, st); break;
-      case PSG_F16: rc = run_dense_keyed<PSG_F16>(s, flags, keys, vals, out, n, st); break;
-      default: rc = run_dense_keyed<PSG_BF16>(s, flags, keys, vals, out, n, st); break;
-    }
-    PSG_TRY(rc);
-    PSG_TRY(read_flags(s, st));
-    PSG_REQUIRE(!s->flags_host[F_UNSORTED], PSG_ERR_INVALID,
-                "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
-    PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE,
-                "request key outside the DENSE store slots [%llu, +%llu) (nothing applied)",
-                (unsigned long long)s->key_begin, (unsigned long long)s->capacity);
-    return PSG_OK;
+  // only a fused keyed request on a populated SORTED store runs in flight;
+  // every other form completes here, in order behind the requests in flight
+  if (s->kind != PSG_STORE_SORTED || !keys || !sorted_fused() || s->size == 0)
+    return handle_sync(s, flags, keys, first_key, vals, out, n, st);
+  if (!s->inflight.empty() && s->inflight.back().stream != st) PSG_TRY(drain(s));  // one stream at a time
+  if (s->inflight.size() >= (size_t)kRing - 1) {
+    int unused = PSG_OK;
+    PSG_TRY(reap(s, s->inflight.front().ticket, 0, &unused));
   }
-  // SORTED
-  PSG_REQUIRE(keys, PSG_ERR_INVALID, "SORTED store needs explicit keys");
-  return sorted_request(s, flags, keys, vals, out, n, st);
+  InflightReq rec;
+  PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec));
+  s->inflight.push_back(rec);
+  *ticket = rec.ticket;
+  return PSG_OK;
+}
+
+int psg_store_wait(psg_store* s, uint64_t ticket) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_wait: null store");
+  int unused = PSG_OK;
+  PSG_TRY(reap(s, ticket ? ticket : ~0ull, 0, &unused));
+  if (s->async_rc != PSG_OK) {
+    const int rc = s->async_rc;
+    s->async_rc = PSG_OK;
+    set_error("%s", s->async_msg.c_str());
+    return rc;
+  }
+  return PSG_OK;
 }
 
 int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert, uint32_t* slots,
@@ -1375,6 +1837,7 @@ int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert
   PSG_REQUIRE(s && slots, PSG_ERR_INVALID, "psg_store_resolve: null argument");
   if (n == 0) return PSG_OK;
   PSG_REQUIRE(keys, PSG_ERR_INVALID, "psg_store_resolve: null keys");
+  PSG_TRY(drain(s));
   hipStream_t st = (hipStream_t)stream;
   if (s->kind == PSG_STORE_DENSE) {
     reset_flags(s);
@@ -1383,7 +1846,7 @@ int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert
     PSG_HIP(hipGetLastError());
     PSG_TRY(read_flags(s, st));
     PSG_REQUIRE(!s->flags_host[F_UNSORTED], PSG_ERR_INVALID,
-                "request keys are not strictly ascending (KVPairs contract, KVApp.h:23)");
+                "slot list keys are not strictly ascending (each key once)");
     PSG_REQUIRE(!s->flags_host[F_RANGE], PSG_ERR_RANGE, "key outside the DENSE store slots");
     return PSG_OK;
   }
@@ -1400,11 +1863,13 @@ int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots, const
   PSG_REQUIRE(slots, PSG_ERR_INVALID, "null slots");
   PSG_REQUIRE(!(flags & PSG_PUSH) || vals, PSG_ERR_INVALID, "push without vals");
   PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
+  PSG_TRY(drain(s));
   return slot_request(s->dtype, flags, s->vals, slots, vals, out, n, (hipStream_t)stream);
 }
 
 int psg_store_dump(psg_store* s, uint64_t* keys_host, void* vals_host) {
   PSG_REQUIRE(s && vals_host, PSG_ERR_INVALID, "psg_store_dump: null argument");
+  PSG_TRY(drain(s));
   PSG_HIP(hipDeviceSynchronize());
   if (s->size == 0) return PSG_OK;
   PSG_HIP(hipMemcpy(vals_host, s->vals, s->size * s->esize, hipMemcpyDeviceToHost));

@@ -443,7 +443,7 @@ struct KVServerDefaultHandle {
       // read (psg.h), so a Push can be answered now; a Pull's reply must land
       // first.  Later requests on this thread's stream are ordered behind it.
       if (req_meta.pull) device::Check(psg_stream_sync(s), "psg_stream_sync");
-      if (state->key_cache) Remember(dkeys, on_dev ? 0 : detail::KeyListHash(req_data.keys.data(), n), s);
+      if (state->key_cache) Remember(dkeys, on_dev, on_dev ? 0 : detail::KeyListHash(req_data.keys.data(), n), s);
     } else if (req_meta.push) {
       CHECK_EQ(n, req_data.vals.size());
     }
@@ -484,15 +484,26 @@ struct KVServerDefaultHandle {
     return *direct ? d : SVector<Value>::OnDevice(n, dev);
   }
 
-  void Remember(const SVector<Key>& dkeys, uint64_t host_hash, psg_stream s) {
+  // worker_frame: dkeys is the request's own HBM frame (the worker's buffer,
+  // or its hipIpc mapping), which the worker may rewrite once the request is
+  // answered (psg.h) — the cache keeps a server-owned copy, as the reference
+  // keeps its received copy (LRServer.h:139), so a later re-resolve never
+  // reads another list, and no worker frame stays mapped.
+  void Remember(const SVector<Key>& dkeys, bool worker_frame, uint64_t host_hash, psg_stream s) {
     const size_t n = dkeys.size();
     uint64_t h = host_hash;
     if (dkeys.on_device() && host_hash == 0)
       device::Check(psg_key_list_hash(dkeys.data(), n, &h, s), "psg_key_list_hash");
     if (state->cache.count(h)) return;
     Cached c;
-    c.keys = dkeys;
-    c.slots = SVector<uint32_t>::OnDevice(n, PostOffice::Get()->device());
+    const int dev = PostOffice::Get()->device();
+    if (worker_frame) {
+      c.keys = SVector<Key>::OnDevice(n, dev);
+      device::Check(psg_memcpy(c.keys.data(), dkeys.data(), n * sizeof(Key), 2 /* D2D */, s), "psg_memcpy D2D");
+    } else {
+      c.keys = dkeys;  // already the server's copy (ToDeviceAsync of a host frame)
+    }
+    c.slots = SVector<uint32_t>::OnDevice(n, dev);
     device::Check(psg_store_resolve(state->store, c.keys.data(), n, 0, c.slots.data(), s), "psg_store_resolve");
     device::Check(psg_stream_sync(s), "psg_stream_sync");
     c.store_size = StoreSize();
@@ -699,9 +710,26 @@ void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const D
         msg.meta.direct_reply = false;
       }
     }
+    bool drop_vals = false;
+    if (direct && !outs) {
+      // a Pull whose vals frame is the caller's output: offered only when this
+      // server's vals slice is the output at its keys' offset (a custom slicer
+      // that copied or remapped the values gets no offer, and a plain Pull
+      // request without values, as the reference sends)
+      const Key* kbase = kvs.keys.data();
+      const Key* k = kv.keys.data();
+      const size_t per = kvs.keys.size() ? kvs.vals.size() / kvs.keys.size() : 0;
+      const bool keys_inside = kv.keys.size() && k >= kbase && k + kv.keys.size() <= kbase + kvs.keys.size();
+      const bool ok = keys_inside && per && kv.vals.size() == kv.keys.size() * per &&
+                      kv.vals.data() == kvs.vals.data() + (size_t)(k - kbase) * per;
+      if (!ok) {
+        msg.meta.direct_reply = false;
+        drop_vals = true;
+      }
+    }
     if (kv.keys.size()) {
       msg.AddData(kv.keys);
-      msg.AddData(kv.vals);
+      msg.AddData(drop_vals ? SVector<Value>() : kv.vals);
       if (kv.lens.size()) msg.AddData(kv.lens);
       if (msg.meta.direct_reply && outs) msg.AddData(out_slice);
     }

@@ -41,11 +41,12 @@ EXPORTS = [
     "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
-    "psg_store_handle", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
+    "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
     "psg_key_list_hash",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
+    "psg_comm_bucket_plan", "psg_comm_keyed_plan",
     "psg_adam_create", "psg_adam_destroy", "psg_lr_apply", "psg_lr_apply_sum",
     "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
@@ -110,6 +111,9 @@ def lib() -> C.CDLL:
             "psg_store_get_info": ([vp, C.POINTER(StoreInfo)], i32),
             "psg_store_clear": ([vp, vp], i32),
             "psg_store_handle": ([vp, i32, vp, u64, vp, vp, u64, vp], i32),
+            "psg_store_handle_async": ([vp, i32, vp, u64, vp, vp, u64, vp, C.POINTER(u64)], i32),
+            "psg_store_wait": ([vp, u64], i32),
+            "psg_sort_pairs_u64": ([vp, vp, u64, i32, vp], i32),
             "psg_store_resolve": ([vp, vp, u64, i32, vp, vp], i32),
             "psg_store_handle_slots": ([vp, i32, vp, vp, vp, u64, vp], i32),
             "psg_store_dump": ([vp, vp, vp], i32),
@@ -118,6 +122,8 @@ def lib() -> C.CDLL:
             "psg_slice": ([vp, u64, vp, u64, i32, vp, vp, vp, vp, vp], i32),
             "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
             "psg_comm_id_bytes": ([], i32), "psg_comm_get_id": ([vp], i32),
+            "psg_comm_bucket_plan": ([u64, i32, vp, vp, i32, C.POINTER(i32)], i32),
+            "psg_comm_keyed_plan": ([vp, i32, u64, C.POINTER(u64)], i32),
             "psg_comm_init": ([vp, i32, i32, C.POINTER(vp)], i32),
             "psg_comm_destroy": ([vp], i32),
             "psg_comm_rank": ([vp, C.POINTER(i32), C.POINTER(i32)], i32),
@@ -343,6 +349,17 @@ class Store:
         _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,
               _s(stream))
 
+    def handle_async(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> int:
+        """Launch without waiting (psg_store_handle_async); returns the ticket (0: done)."""
+        t = C.c_uint64(0)
+        _call("psg_store_handle_async", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,
+              _s(stream), C.byref(t))
+        return t.value
+
+    def wait(self, ticket: int = 0) -> None:
+        """Complete the requests in flight up to `ticket` (0: all); raises the first failure."""
+        _call("psg_store_wait", self.h, ticket)
+
     def resolve(self, keys, n: int, slots, insert: bool = True, stream=None) -> None:
         _call("psg_store_resolve", self.h, _ptr(keys), n, int(insert), _ptr(slots), _s(stream))
 
@@ -410,6 +427,30 @@ def comm_id() -> bytes:
     buf = C.create_string_buffer(n)
     _call("psg_comm_get_id", buf)
     return buf.raw
+
+
+def sort_pairs_u64(keys, vals, n: int, bits: int = 64, stream=None) -> None:
+    """Stable device radix sort of (keys, vals) by the low `bits` of the key, in place."""
+    _call("psg_sort_pairs_u64", _ptr(keys), _ptr(vals), n, bits, _s(stream))
+
+
+def bucket_plan(blk: int, nbuckets: int):
+    """(offsets, counts) of psg_comm_push_pull's buckets over a block of blk
+    elements (host-only: the same numbers the RCCL pipeline uses)."""
+    offs = np.zeros(max(nbuckets, 1), np.uint64)
+    cnts = np.zeros(max(nbuckets, 1), np.uint64)
+    nb = C.c_int(0)
+    _call("psg_comm_bucket_plan", blk, nbuckets, offs.ctypes.data_as(C.c_void_p),
+          cnts.ctypes.data_as(C.c_void_p), len(offs), C.byref(nb))
+    return offs[:nb.value].copy(), cnts[:nb.value].copy()
+
+
+def keyed_plan(key_pos, nranks: int, n: int) -> int:
+    """psg_comm_push_keyed's check of the slicer bounds; returns the longest segment."""
+    kp = np.ascontiguousarray(key_pos, dtype=np.uint64)
+    m = C.c_uint64(0)
+    _call("psg_comm_keyed_plan", kp.ctypes.data_as(C.c_void_p), nranks, n, C.byref(m))
+    return m.value
 
 
 class Comm:

@@ -61,7 +61,12 @@ def default_rendezvous_file() -> str:
 class SocketGroup:
     """barrier / broadcast / all_gather / allreduce_max over a loopback star."""
 
-    def __init__(self, rank: int, world: int, path: str | None = None, timeout_s: float = 300.0):
+    def __init__(self, rank: int, world: int, path: str | None = None, timeout_s: float | None = None):
+        # every rendezvous and every later collective waits at most timeout_s
+        # (PSG_GROUP_TIMEOUT_S, default 180 s) for a peer, then raises: a rank
+        # that died or hangs ends the job with an error instead of a hang
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("PSG_GROUP_TIMEOUT_S", "180"))
         self.rank, self.world = rank, world
         self.path = path or default_rendezvous_file()
         self.peers: list[socket.socket] = []

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -336,7 +337,10 @@ namespace {
 // Spawning the helper threads per call cost more than the copy it split: a
 // 16 MiB staging chunk copied by 4 fresh threads spent ~25 us on thread
 // creation and join alone.  One job at a time; the caller runs part 0 and
-// the workers take the rest by an atomic ticket.  Never destroyed: its
+// the workers take the rest by an atomic ticket OF THAT JOB: every job has its
+// own ticket and part counters, and a worker drains only the job it took
+// under the lock, so a worker still leaving an old job can never run a part
+// of the next one (or count one of its parts twice).  Never destroyed: its
 // threads may still be parked when static destructors run.
 class CopyPool {
  public:
@@ -345,54 +349,59 @@ class CopyPool {
   }
   void Run(char* dst, const char* src, size_t bytes, int parts, size_t chunk) {
     std::lock_guard<std::mutex> job_lk(job_mu_);
+    auto job = std::make_shared<Job>();
+    job->dst = dst;
+    job->src = src;
+    job->bytes = bytes;
+    job->chunk = chunk;
+    job->parts = parts;
+    job->left.store(parts, std::memory_order_relaxed);
     {
-      // a worker still in Drain from the last job may take a ticket of this
-      // one as soon as next_ is reset: publish everything else first
       std::lock_guard<std::mutex> lk(mu_);
-      left_.store(parts, std::memory_order_relaxed);
-      dst_ = dst;
-      src_ = src;
-      bytes_ = bytes;
-      chunk_ = chunk;
-      parts_ = parts;
-      next_.store(1, std::memory_order_release);
+      job_ = job;
       ++gen_;
     }
     cv_.notify_all();
-    Part(0);
-    Drain();
-    // the workers may still be taking tickets past the end: wait for all parts
-    while (left_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    Part(*job, 0);
+    Drain(*job);
+    // every part of THIS job done (a worker that took a ticket may still be
+    // copying its part: wait for the count, not for the tickets)
+    while (job->left.load(std::memory_order_acquire) != 0) std::this_thread::yield();
   }
 
  private:
-  void Part(int i) {
-    const size_t off = chunk_ * (size_t)i;
-    if (off < bytes_) std::memcpy(dst_ + off, src_ + off, std::min(chunk_, bytes_ - off));
-    left_.fetch_sub(1, std::memory_order_acq_rel);
+  struct Job {
+    char* dst = nullptr;
+    const char* src = nullptr;
+    size_t bytes = 0, chunk = 0;
+    int parts = 0;
+    std::atomic<int> next{1}, left{0};
+  };
+  static void Part(Job& j, int i) {
+    const size_t off = j.chunk * (size_t)i;
+    if (off < j.bytes) std::memcpy(j.dst + off, j.src + off, std::min(j.chunk, j.bytes - off));
+    j.left.fetch_sub(1, std::memory_order_acq_rel);
   }
-  void Drain() {
-    for (int i; (i = next_.fetch_add(1, std::memory_order_acq_rel)) < parts_;) Part(i);
+  static void Drain(Job& j) {
+    for (int i; (i = j.next.fetch_add(1, std::memory_order_acq_rel)) < j.parts;) Part(j, i);
   }
   void Work() {
     uint64_t seen = 0;
     for (;;) {
+      std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
+        j = job_;
       }
-      Drain();
+      if (j) Drain(*j);
     }
   }
   std::mutex job_mu_, mu_;
   std::condition_variable cv_;
   uint64_t gen_ = 0;
-  char* dst_ = nullptr;
-  const char* src_ = nullptr;
-  size_t bytes_ = 0, chunk_ = 0;
-  int parts_ = 0;
-  std::atomic<int> next_{0}, left_{0};
+  std::shared_ptr<Job> job_;
 };
 }  // namespace
 

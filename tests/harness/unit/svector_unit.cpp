@@ -3,6 +3,7 @@
 // std::vector, sharing copies, non-owning wraps, Slice aliasing and
 // detach-on-growth (SliceTest, :411-462), resize/fill, reinterpreting views,
 // FindRange.  Plain program (no PS node): exits non-zero on a failed CHECK.
+#include <atomic>
 #include <cstdio>
 #include <cstdint>
 #include <memory>
@@ -111,6 +112,25 @@ int main() {
     std::vector<std::thread> ts;
     for (uint32_t t = 0; t < 4; ++t) ts.emplace_back([&, t] { for (int r = 0; r < 3; ++r) check_big((size_t(9) << 20) + 777 * t, t * 100 + r); });
     for (auto& t : ts) t.join();
+  }
+  {  // HostCopy stress: back-to-back jobs of varying sizes from 8 threads at
+     // once (more callers than copy workers), every byte checked.  A worker
+     // still leaving job k must never run a part of job k + 1, or a job could
+     // return while one of its parts is still being copied.
+    std::vector<std::thread> ts;
+    std::atomic<int> bad{0};
+    for (uint32_t t = 0; t < 8; ++t)
+      ts.emplace_back([&, t] {
+        for (int r = 0; r < 24; ++r) {
+          const size_t n = (size_t(4) << 20) / 4 + (size_t)((t * 7919u + r * 104729u) % (3u << 20));
+          std::vector<uint32_t> src(n), dst(n, 0xdeadbeefu);
+          for (size_t i = 0; i < n; ++i) src[i] = (uint32_t)(i * 2246822519u) ^ (t << 24) ^ (uint32_t)r;
+          ps::HostCopy(dst.data(), src.data(), n * 4);
+          if (dst != src) bad.fetch_add(1);
+        }
+      });
+    for (auto& t : ts) t.join();
+    CHECK_EQ(bad.load(), 0) << "HostCopy returned before its copy was complete";
   }
   std::printf("svector ok\n");
   return 0;

@@ -226,3 +226,116 @@ def test_lr_bsp_reduce_scatter_within_tolerance(world):
         exp[s * blk:(s + 1) * blk] = w
     for r in range(world):
         assert np.all(np.abs(got[r] - exp) <= REL_TOL * np.abs(exp) + 1e-7), r
+
+
+# ---------------------------------------------------------------------------
+# The RCCL exchanges that only ever ran with one rank on the GPU box —
+# psg_comm_push_keyed / _pull_keyed (configs[3]) and psg_comm_push_pull's
+# bucket pipeline — rehearsed with 2-4 ranks on gloo.  The offsets come from
+# the same code the RCCL path runs: the library's host-only plans
+# (psg_comm_keyed_plan, psg_comm_bucket_plan) and its server ranges
+# (psg_server_ranges, PostOffice.cpp:211-221); the slice is the oracle's
+# DefaultSlicer restatement (KVApp.h:515-574), which the -m gpu tests pin to
+# psg_slice.  Each owner applies its reduced segment with oracle.Store, the
+# CPU restatement of the handle the GPU path calls (psg_store_handle).
+# Integer-valued data: bit-exact (every partial sum is exact in f32);
+# real-valued: the north star's 1e-6 relative (the reduce sums in its own order).
+def _exchange_rank(rank, world, port, outdir, kind, data):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "parameter-server_amd", "python")]
+    import torch
+    import torch.distributed as dist
+    import oracle
+    import psg
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    mode, lo, hi = (0, 0.0, 1000.0) if data == "int" else (1, -1.0, 1.0)
+    steps = 3
+    if kind == "keyed":
+        rng = np.random.default_rng(5)
+        keys = np.unique(rng.integers(0, (1 << 64) - 1, 30000, dtype=np.uint64))
+        n = len(keys)
+        b, e = psg.server_ranges(world)
+        ob, oe = oracle.server_ranges(world)
+        assert np.array_equal(b, ob) and np.array_equal(e, oe)
+        kp, _ = oracle.slice_keys(keys, b, e)
+        kp = [int(x) for x in kp]
+        maxseg = psg.keyed_plan(kp, world, n)
+        assert all(kp[r + 1] - kp[r] <= maxseg for r in range(world))
+        vals = torch.from_numpy(oracle.synth(n, oracle.F32, 50 + rank, mode, lo, hi))
+        store = oracle.Store(oracle.F32)
+        mine = keys[kp[rank]:kp[rank + 1]]
+        for _ in range(steps):
+            for r in range(world):  # one reduce per key-range segment, to its owner
+                seg = vals[kp[r]:kp[r + 1]].clone()
+                dist.reduce(seg, dst=r)
+                if r == rank and len(mine):
+                    store.handle(oracle.PUSH, mine, seg.numpy(), len(mine))
+        out = torch.zeros(n, dtype=torch.float32)
+        if len(mine):
+            out[kp[rank]:kp[rank + 1]] = torch.from_numpy(store.handle(oracle.PULL, mine, None, len(mine)))
+        for r in range(world):  # each owner broadcasts its segment into place
+            view = out[kp[r]:kp[r + 1]]
+            if view.numel():
+                dist.broadcast(view, src=r)
+    else:
+        blk = 10007  # not a multiple of 64: a ragged last bucket
+        L = blk * world
+        vals = torch.from_numpy(oracle.synth(L, oracle.F32, 70 + rank, mode, lo, hi))
+        shard = torch.zeros(blk, dtype=torch.float32)
+        out = torch.zeros(L, dtype=torch.float32)
+        for step, nb in enumerate([1, 3, 8][:steps]):
+            offs, cnts = psg.bucket_plan(blk, nb)
+            assert int(offs[0]) == 0 and int(offs[-1] + cnts[-1]) == blk
+            assert all(int(offs[i + 1]) == int(offs[i] + cnts[i]) for i in range(len(offs) - 1))
+            for off, cnt in zip((int(x) for x in offs), (int(x) for x in cnts)):
+                for r in range(world):  # bucket b of every rank's block, reduced to its owner
+                    red = vals[r * blk + off:r * blk + off + cnt].clone()
+                    dist.reduce(red, dst=r)
+                    if r == rank:
+                        shard[off:off + cnt] += red
+                for r in range(world):  # ... and broadcast back from the owner
+                    view = out[r * blk + off:r * blk + off + cnt]
+                    if r == rank:
+                        view.copy_(shard[off:off + cnt])
+                    dist.broadcast(view, src=r)
+    np.save(os.path.join(outdir, f"x{rank}.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("data", ["int", "real"])
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("kind", ["keyed", "buckets"])
+def test_rccl_exchange_plans_rehearsed_on_gloo(kind, world, data):
+    import multiprocessing as mp
+    sys.path[:0] = [os.path.join(ROOT, "oracle")]
+    import oracle
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as d:
+        port = _free_port()
+        procs = [ctx.Process(target=_exchange_rank, args=(r, world, port, d, kind, data)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        got = [np.load(os.path.join(d, f"x{r}.npy")) for r in range(world)]
+    mode, lo, hi = (0, 0.0, 1000.0) if data == "int" else (1, -1.0, 1.0)
+    ref = oracle.Store(oracle.F32)
+    if kind == "keyed":
+        keys = np.unique(np.random.default_rng(5).integers(0, (1 << 64) - 1, 30000, dtype=np.uint64))
+        n = len(keys)
+        for _ in range(3):  # every worker's Push, in worker order (KVApp.h:446-454)
+            for w in range(world):
+                ref.handle(oracle.PUSH, keys, oracle.synth(n, oracle.F32, 50 + w, mode, lo, hi), n)
+        exp = ref.handle(oracle.PULL, keys, None, n)
+    else:
+        L = 10007 * world
+        for _ in range(3):
+            for w in range(world):
+                ref.handle(oracle.PUSH, None, oracle.synth(L, oracle.F32, 70 + w, mode, lo, hi), L)
+        exp = ref.handle(oracle.PULL, None, None, L)
+    for r in range(world):
+        if data == "int":
+            np.testing.assert_array_equal(got[r], exp, err_msg=f"rank {r}")
+        else:
+            assert np.all(np.abs(got[r] - exp) <= REL_TOL * np.abs(exp) + 1e-6), r

@@ -100,6 +100,21 @@ def test_default_handle_key_cache_end_to_end(nw):
     assert len(lines) == nw and all(l["key_cache"] == 1 for l in lines)
 
 
+@pytest.mark.parametrize("procs", [False, True])
+def test_reference_semantics_through_the_cpp_api(procs):
+    """tests/harness/kv_semantics_device.cpp: keys out of order and repeated
+    (HBM frames and host vectors) answered like KVApp.h:446-454's loop; the key
+    cache keeps its own copy of a list the worker then rewrites in place; a
+    copying custom slicer gets no direct-reply offer, so the merged reply fills
+    the caller's output."""
+    exe = os.path.join(BIN, "kv_semantics_device")
+    _need(exe)
+    r = run(exe, "-ns", 1, "-nw", 1, *(["-procs"] if procs else []))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    for what in ("out-of-order ok", "key cache ok", "custom slicer ok"):
+        assert what in r.stdout
+
+
 @pytest.mark.parametrize("ns,nw,direct", [(1, 1, True), (2, 2, True), (2, 2, False)])
 def test_device_frames_end_to_end(ns, nw, direct):
     """HBM ZPush / ZPull / ZPushPull through the C++ API, every value checked.

@@ -224,53 +224,236 @@ def test_sorted_extreme_keys_and_empty_request():
     assert st.info().size == 4
 
 
-def test_sorted_rejects_duplicate_keys():
+def test_sorted_duplicate_keys_apply_in_arrival_order():
+    """The reference's loop (KVApp.h:446-454) adds each occurrence of a key in
+    turn and a PushPull answers each occurrence with the running value."""
     st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
-    with pytest.raises(psg.PsgError) as ei:
-        st.handle(psg.PUSH, dev(np.array([5, 7, 7, 9], np.uint64)), dev(np.ones(4, np.float32)),
-                  None, 4)
-    assert ei.value.code == 1 and "ascending" in str(ei.value)
+    orc = oracle.Store()
+    k = np.array([5, 7, 7, 9], np.uint64)
+    v = np.array([1.0, 2.0, 3.0, 4.0], np.float32)
+    out = psg.DeviceBuffer(16)
+    for flags in (psg.PUSH, psg.PUSH | psg.PULL, psg.PULL):
+        st.handle(flags, dev(k), dev(v), out, 4)
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, 4)
+        if flags & psg.PULL:
+            np.testing.assert_array_equal(out.download(np.float32, 4), exp)
+    np.testing.assert_array_equal(out.download(np.float32, 4), [2.0, 10.0, 10.0, 8.0])
+
+
+def _disorder(univ, bad, rng):
+    k = univ.copy()
+    if bad == "duplicate_last_tile":
+        k[-3] = k[-4]
+    elif bad == "unsorted_middle":
+        k[30000], k[30001] = k[30001], k[30000]
+    elif bad == "duplicate_adjacent_lanes":
+        k[4100] = k[4099]  # the last key of lane 0 and the first of lane 1, second tile
+    elif bad == "duplicate_adjacent_waves":
+        k[4096 + 256] = k[4096 + 255]  # the last key of wave 0 and the first of wave 1
+    elif bad == "shuffled":
+        rng.shuffle(k)
+    elif bad == "hot_keys":  # a few keys repeated many times, the rest once
+        k[rng.integers(0, len(k), len(k) // 4)] = k[rng.integers(0, 16, len(k) // 4)]
+    elif bad == "reversed":
+        k = k[::-1].copy()
+    return k
 
 
 @pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL])
-@pytest.mark.parametrize("bad", ["duplicate_last_tile", "unsorted_middle", "out_of_range_last",
-                                 "duplicate_adjacent_lanes", "duplicate_adjacent_waves"])
-def test_sorted_rejected_request_leaves_a_populated_store_unchanged(bad, flags):
-    """The KVPairs contract (KVApp.h:23): keys strictly ascending.  A request that
-    breaks it — or names a key outside the shard — is rejected as a whole
-    (k_validate_windows runs over every key before k_resolve_apply writes), so
-    the store keeps exactly what it held, even when the bad key sits in the
-    last of many request tiles.  A Pull checks its keys inside k_resolve_apply
-    (lane to lane by a shuffle, wave to wave by a load) and is rejected before
-    any absent key is inserted."""
+@pytest.mark.parametrize("bad", ["duplicate_last_tile", "unsorted_middle", "duplicate_adjacent_lanes",
+                                 "duplicate_adjacent_waves", "shuffled", "hot_keys", "reversed"])
+def test_sorted_out_of_order_request_on_a_populated_store(bad, flags):
+    """Keys out of order or repeated — wherever the break sits: the last of many
+    tiles, between lanes, between waves — are detected by the fast path's
+    checks (k_validate_windows; a Pull inside k_resolve_apply), which then
+    write nothing; the request is served by the order-preserving path (stable
+    device sort by slot + one lane per key) bit-exactly like the reference's
+    sequential loop, and absent keys among them are inserted once."""
+    rng = np.random.default_rng(41)
+    kb, ke = 1000, 1 << 62
+    univ = np.unique(rng.integers(kb, ke, 60000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, psg.F32, kb, ke, 0)
+    orc = oracle.Store()
+    v0 = rng.uniform(-1, 1, len(univ)).astype(np.float32)
+    st.handle(psg.PUSH, dev(univ[::2]), dev(v0[::2]), None, len(univ[::2]))  # half present
+    orc.handle(oracle.PUSH, univ[::2], v0[::2], len(univ[::2]))
+    k = _disorder(univ, bad, rng)
+    n = len(k)
+    v = rng.uniform(-1, 1, n).astype(np.float32)
+    out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+    for _ in range(2):
+        st.handle(flags, dev(k), dev(v) if flags & psg.PUSH else None, out, n)
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
+        if out is not None:
+            np.testing.assert_array_equal(out.download(np.float32, n), exp)
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv, ov)
+    # and the fast path still serves sorted requests afterwards
+    st.handle(psg.PUSH, dev(univ), dev(np.ones(len(univ), np.float32)), None, len(univ))
+    orc.handle(oracle.PUSH, univ, np.ones(len(univ), np.float32), len(univ))
+    np.testing.assert_array_equal(st.dump()[1], orc.dump()[1])
+
+
+@pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL])
+def test_sorted_out_of_range_request_leaves_a_populated_store_unchanged(flags):
+    """A key outside the shard's range rejects the request as a whole
+    (k_validate_windows reads every key before k_resolve_apply writes): the
+    store keeps exactly what it held, even when the bad key is the last of
+    many tiles and the request is also out of order."""
     rng = np.random.default_rng(41)
     kb, ke = 1000, 1 << 62
     univ = np.unique(rng.integers(kb, ke, 60000, dtype=np.uint64))
     st = psg.Store(psg.SORTED, psg.F32, kb, ke, 0)
     st.handle(psg.PUSH, dev(univ), dev(rng.uniform(-1, 1, len(univ)).astype(np.float32)), None, len(univ))
     k0, v0 = st.dump()
-    k = univ.copy()
-    if bad == "duplicate_last_tile":
-        k[-3] = k[-4]
-    elif bad == "unsorted_middle":
-        k[30000], k[30001] = k[30001], k[30000]
-    elif bad == "out_of_range_last":
+    for variant in ("last", "last_and_unsorted"):
+        k = univ.copy()
         k[-1] = ke + 5
-    elif bad == "duplicate_adjacent_lanes":
-        k[4100] = k[4099]  # the last key of lane 0 and the first of lane 1, second tile
-    else:
-        k[4096 + 256] = k[4096 + 255]  # the last key of wave 0 and the first of wave 1
-    n = len(k)
-    out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
-    with pytest.raises(psg.PsgError) as ei:
-        st.handle(flags, dev(k), dev(np.ones(n, np.float32)), out, n)
-    assert ei.value.code == (4 if bad.startswith("out_of_range") else 1)
-    k1, v1 = st.dump()
-    np.testing.assert_array_equal(k1, k0)
-    np.testing.assert_array_equal(v1, v0)
-    # and the store still serves requests
+        if variant == "last_and_unsorted":
+            k[100], k[101] = k[101], k[100]
+        n = len(k)
+        out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+        with pytest.raises(psg.PsgError) as ei:
+            st.handle(flags, dev(k), dev(np.ones(n, np.float32)), out, n)
+        assert ei.value.code == 4
+        k1, v1 = st.dump()
+        np.testing.assert_array_equal(k1, k0)
+        np.testing.assert_array_equal(v1, v0)
     st.handle(psg.PUSH, dev(univ), dev(np.ones(len(univ), np.float32)), None, len(univ))
     np.testing.assert_array_equal(st.dump()[1], (v0 + np.float32(1)).astype(np.float32))
+
+
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64, psg.F16, psg.BF16])
+@pytest.mark.parametrize("kind", ["sorted_empty", "sorted_populated", "dense"])
+def test_shuffled_and_repeated_keys_all_dtypes(dtype, kind):
+    """Requests with shuffled keys and runs of duplicates, in all four dtypes,
+    on an empty SORTED store (the first request inserts), a populated one, and
+    a DENSE store addressed by keys: Push, PushPull and Pull bit-exact against
+    oracle.Store, the sequential unordered_map loop of KVApp.h:446-454."""
+    rng = np.random.default_rng(7 + dtype)
+    if kind == "dense":
+        kb, cap = 100, 50000
+        st = psg.Store(psg.DENSE, dtype, kb, kb + cap, cap)
+        univ = np.arange(kb, kb + cap, dtype=np.uint64)
+    else:
+        st = psg.Store(psg.SORTED, dtype, 0, KMAX, 0)
+        univ = np.unique(rng.integers(0, KMAX, 80000, dtype=np.uint64))
+    orc = oracle.Store(dtype)
+    if kind != "sorted_empty":
+        w = synth(len(univ), dtype, 5, 1, -1.0, 1.0)
+        st.handle(psg.PUSH, dev(univ), dev(w), None, len(univ))
+        orc.handle(oracle.PUSH, univ, w, len(univ))
+    for j in range(6):
+        n = int(rng.integers(1, 120000))
+        k = rng.choice(univ, n, replace=True)  # repeats, any order
+        if j % 2:
+            k[: n // 3] = k[0]  # a long run of one key
+            rng.shuffle(k)
+        flags = [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL][j % 3]
+        v = synth(n, dtype, 100 + j, 1, -1.0, 1.0)
+        out = psg.DeviceBuffer(n * ES[dtype]) if flags & psg.PULL else None
+        st.handle(flags, dev(k), dev(v) if flags & psg.PUSH else None, out, n)
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
+        if out is not None:
+            np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"request {j}")
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    if kind == "dense":  # every slot of a DENSE store exists; the untouched ones stay 0
+        g = gv.view(NPT[dtype])
+        idx = (ok - np.uint64(kb)).astype(np.int64)
+        np.testing.assert_array_equal(g[idx], ov.view(NPT[dtype]))
+        rest = np.ones(len(g), bool)
+        rest[idx] = False
+        assert not np.any(g[rest].view(np.uint8))
+    else:
+        np.testing.assert_array_equal(gk, ok)
+        np.testing.assert_array_equal(gv.view(NPT[dtype]), ov)
+
+
+@pytest.mark.parametrize("n", [1, 17, 4096, 4097, 100003, 3_000_000])
+@pytest.mark.parametrize("bits", [8, 20, 64])
+def test_device_radix_sort_is_stable(n, bits):
+    """psg_sort.hip against numpy's stable argsort on the low `bits` of the key."""
+    rng = np.random.default_rng(n + bits)
+    k = rng.integers(0, 1 << 63, n, dtype=np.uint64) | (rng.integers(0, 2, n, dtype=np.uint64) << np.uint64(63))
+    if n > 100:
+        k[: n // 5] = k[0]  # many equal keys: stability matters
+    v = np.arange(n, dtype=np.uint32)
+    dk, dv = dev(k), dev(v)
+    psg.sort_pairs_u64(dk, dv, n, bits)
+    psg.device_sync()
+    key = k & np.uint64((1 << bits) - 1) if bits < 64 else k
+    order = np.argsort(key, kind="stable")
+    np.testing.assert_array_equal(dv.download(np.uint32, n), v[order])
+    np.testing.assert_array_equal(dk.download(np.uint64, n), k[order])
+
+
+@pytest.mark.parametrize("depth", [1, 4, 40])
+def test_async_requests_with_absent_keys_replay_in_order(depth):
+    """psg_store_handle_async: a stream of requests in flight on a populated
+    store, many of which carry a few absent keys (or keys out of order).  Each
+    such request raises the store's pending word; every request launched
+    behind it writes nothing and reports itself gated; the wait inserts the
+    keys and replays them in order.  The whole sequence — Push, PushPull and
+    Pull mixed — is bit-exact against the oracle, with at most `depth`
+    requests in flight."""
+    rng = np.random.default_rng(99 + depth)
+    univ = np.unique(rng.integers(0, KMAX, 200000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    base = univ[: len(univ) // 2]
+    w = rng.uniform(-1, 1, len(base)).astype(np.float32)
+    st.handle(psg.PUSH, dev(base), dev(w), None, len(base))
+    orc.handle(oracle.PUSH, base, w, len(base))
+    reqs, pending = [], []
+    for j in range(60):
+        if j % 5 == 0:  # a few keys the store has not seen yet
+            extra = rng.choice(univ[len(univ) // 2:], 7, replace=False)
+            k = np.unique(np.concatenate([base[j * 100:(j + 1) * 100 + 5000], extra]))
+        elif j % 11 == 3:  # out of order
+            k = base[j * 50:j * 50 + 3000].copy()
+            rng.shuffle(k)
+        else:
+            k = base[(j * 997) % 50000:(j * 997) % 50000 + 20000]
+        flags = [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL][j % 3]
+        v = rng.uniform(-1, 1, len(k)).astype(np.float32)
+        dk, dv = dev(k), dev(v)
+        out = psg.DeviceBuffer(len(k) * 4) if flags & psg.PULL else None
+        t = st.handle_async(flags, dk, dv if flags & psg.PUSH else None, out, len(k))
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, len(k))
+        reqs.append((dk, dv, out, exp, len(k)))
+        pending.append(t)
+        if len(pending) >= depth:
+            st.wait(pending.pop(0))
+    st.wait()
+    psg.device_sync()
+    for j, (_, _, out, exp, n) in enumerate(reqs):
+        if out is not None:
+            np.testing.assert_array_equal(out.download(np.float32, n), exp, err_msg=f"request {j}")
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv, ov)
+
+
+def test_async_request_failure_is_reported_by_wait():
+    st = psg.Store(psg.SORTED, psg.F32, 0, 1 << 40, 0)
+    k = np.arange(1000, dtype=np.uint64) * 7
+    st.handle(psg.PUSH, dev(k), dev(np.ones(1000, np.float32)), None, 1000)
+    bad = k.copy()
+    bad[-1] = 1 << 41  # outside [0, 2^40)
+    dk, db = dev(k), dev(bad)
+    ones = dev(np.ones(1000, np.float32))
+    t1 = st.handle_async(psg.PUSH, db, ones, None, 1000)
+    t2 = st.handle_async(psg.PUSH, dk, ones, None, 1000)
+    assert t1 and t2 > t1
+    with pytest.raises(psg.PsgError) as ei:
+        st.wait(t2)
+    assert ei.value.code == 4
+    st.wait()  # reported once
+    np.testing.assert_array_equal(st.dump()[1], np.full(1000, 2.0, np.float32))
 
 
 @pytest.mark.parametrize("dtype", [psg.F32, psg.F64])
@@ -309,7 +492,9 @@ def test_sorted_window_cache_transitions(dtype):
         exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
         if flags & psg.PULL:
             np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"request {j}")
-    # a Pull with one unsorted pair on trusted windows is rejected, store unchanged
+    # a Pull with one unsorted pair on trusted windows: k_resolve_apply's own
+    # check catches it and the order-preserving path answers it; the store is
+    # unchanged, and the trusted windows still serve the sorted list after
     dk.upload(a)
     st.handle(psg.PULL, dk, None, out, n)
     st.handle(psg.PULL, dk, None, out, n)
@@ -317,19 +502,21 @@ def test_sorted_window_cache_transitions(dtype):
     bad[n // 2], bad[n // 2 + 1] = bad[n // 2 + 1], bad[n // 2]
     dk.upload(bad)
     k0, s0 = st.dump()
-    with pytest.raises(psg.PsgError) as ei:
-        st.handle(psg.PULL, dk, None, out, n)
-    assert ei.value.code == 1
+    st.handle(psg.PULL, dk, None, out, n)
+    np.testing.assert_array_equal(out.download(NPT[dtype], n), orc.handle(oracle.PULL, bad, None, n))
     k1, s1 = st.dump()
     np.testing.assert_array_equal(k1, k0)
     np.testing.assert_array_equal(s1, s0)
+    dk.upload(a)
+    st.handle(psg.PULL, dk, None, out, n)
+    np.testing.assert_array_equal(out.download(NPT[dtype], n), orc.handle(oracle.PULL, a, None, n))
     gk, gv = st.dump()
     ok, ov = orc.dump()
     np.testing.assert_array_equal(gk, ok)
     np.testing.assert_array_equal(gv.view(NPT[dtype]), ov)
 
 
-def test_dense_keyed_rejected_request_leaves_the_store_unchanged():
+def test_dense_keyed_out_of_range_rejected_out_of_order_applied():
     st = psg.Store(psg.DENSE, psg.F32, 100, 100000, 5000)
     base = np.arange(5000, dtype=np.float32)
     st.handle(psg.PUSH, None, dev(base), None, 5000, first_key=100)
@@ -339,12 +526,18 @@ def test_dense_keyed_rejected_request_leaves_the_store_unchanged():
         st.handle(psg.PUSH, dev(keys), dev(np.ones(5000, np.float32)), None, 5000)
     assert ei.value.code == 4
     np.testing.assert_array_equal(st.dump()[1], base)
+    # out of order and repeated keys are applied in arrival order, like the
+    # reference's loop, on the DENSE store too
     keys = np.arange(100, 5100, dtype=np.uint64)
     keys[10], keys[11] = keys[11], keys[10]
-    with pytest.raises(psg.PsgError) as ei:
-        st.handle(psg.PUSH, dev(keys), dev(np.ones(5000, np.float32)), None, 5000)
-    assert ei.value.code == 1
-    np.testing.assert_array_equal(st.dump()[1], base)
+    keys[20] = keys[21]
+    ones = np.ones(5000, np.float32)
+    out = psg.DeviceBuffer(5000 * 4)
+    st.handle(psg.PUSH | psg.PULL, dev(keys), dev(ones), out, 5000)
+    orc = oracle.Store()
+    orc.handle(oracle.PUSH, np.arange(100, 5100, dtype=np.uint64), base, 5000)
+    np.testing.assert_array_equal(out.download(np.float32, 5000), orc.handle(oracle.PUSH | oracle.PULL, keys, ones, 5000))
+    np.testing.assert_array_equal(st.dump()[1], orc.dump()[1][np.argsort(orc.dump()[0])])
 
 
 _RA_BLOCK_CHILD = """
@@ -396,12 +589,13 @@ def test_dense_store_resolve_slots():
         st.resolve(dev(np.array([100, 600], np.uint64)), 2, slots)
 
 
-def test_sorted_rejects_unsorted_and_out_of_range():
+def test_sorted_small_out_of_order_and_out_of_range():
     st = psg.Store(psg.SORTED, psg.F32, 100, 200, 0)
     v = dev(np.ones(3, np.float32))
-    with pytest.raises(psg.PsgError) as ei:
-        st.handle(psg.PUSH, dev(np.array([150, 120, 160], np.uint64)), v, None, 3)
-    assert ei.value.code == 1
+    st.handle(psg.PUSH, dev(np.array([150, 120, 160], np.uint64)), v, None, 3)  # the first request: two-pass form
+    st.handle(psg.PUSH, dev(np.array([160, 150, 150], np.uint64)), v, None, 3)  # fused form
+    k, vals = st.dump()
+    assert k.tolist() == [120, 150, 160] and vals.tolist() == [1.0, 3.0, 2.0]
     with pytest.raises(psg.PsgError) as ei:
         st.handle(psg.PUSH, dev(np.array([150, 199, 200], np.uint64)), v, None, 3)
     assert ei.value.code == 4
@@ -556,6 +750,39 @@ def test_comm_single_rank_push_pull(force, dtype, n, monkeypatch):
         exp = orc.handle(oracle.PUSH | oracle.PULL, None, hv, n)
         np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"nbuckets={nb}")
     c.close()
+
+
+_NEVER_JOINS = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import psg
+psg.set_device(0)
+uid = psg.comm_id()
+t0 = time.monotonic()
+try:
+    psg.Comm(uid, 2, 0)  # rank 1 of this world-2 communicator never joins
+    print("JOINED")
+except psg.PsgError as e:
+    print("FAILED", e.code, round(time.monotonic() - t0, 2), str(e))
+"""
+
+
+def test_comm_init_with_a_rank_that_never_joins_fails_within_the_deadline():
+    """psg_comm_init meets the other ranks on a non-blocking probe communicator
+    polled against PSG_COMM_TIMEOUT_S: a world-2 communicator whose rank 1
+    never arrives fails with PSG_ERR_COMM after the deadline instead of
+    hanging the job (run in a child process, under a hard limit of its own)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, PSG_COMM_TIMEOUT_S="6")
+    r = subprocess.run([sys.executable, "-c", _NEVER_JOINS, os.path.dirname(psg.__file__)],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith(("FAILED", "JOINED"))][-1]
+    words = line.split()
+    assert words[0] == "FAILED" and int(words[1]) == 5, line
+    assert 5.0 <= float(words[2]) <= 40.0, line  # the deadline, not a hang
+    assert "did not join" in line
 
 
 @pytest.mark.parametrize("nbytes", [0, 8, 4096, 8 * 1000003])

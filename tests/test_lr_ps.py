@@ -112,6 +112,25 @@ def _closest_replay(parts, got, nw):
 
 @pytest.mark.parametrize("nw,key_cache", [(1, False), (4, False), (4, True)])
 def test_reference_lr_ps_trains_on_this_runtime(tmp_path, nw, key_cache):
+    _run_lr_ps(tmp_path, nw, key_cache)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nw,key_cache", [(4, False), (4, True)])
+def test_reference_lr_ps_trains_on_the_mi355x_box(tmp_path, nw, key_cache):
+    """The same unmodified LR_ps.cpp on the GPU box: every node process then
+    opens the GPU (node k of each role on GPU k % ngpu), its large frames come
+    from the pinned pool and the Van runs with HIP up; the reference's own
+    LRServer handle is a host handle (SetRequestHandle), so the model math
+    stays the reference's, and the replay bar is the same."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "parameter-server_amd", "python"))
+    import psg
+    assert psg.device_count() >= 1, "no GPU visible"
+    _run_lr_ps(tmp_path, nw, key_cache)
+
+
+def _run_lr_ps(tmp_path, nw, key_cache):
     if not os.path.exists(EXE):
         pytest.skip(f"{EXE} not built (needs the reference tree)")
     rng = np.random.default_rng(12)
