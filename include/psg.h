@@ -258,7 +258,10 @@ int psg_server_ranges(int num_servers, uint64_t* begins_host, uint64_t* ends_hos
  *                  (the running sum of KVApp.h:565-569; val_pos[0] = 0).
  * key_pos_host / val_pos_host hold ns + 1 entries (val_pos_host may be NULL).
  * Fails (PSG_ERR_INVALID) when key_pos[ns] != n, i.e. a key lies at or above
- * the last range's end (the CHECK at KVApp.h:544).  Synchronises the stream. */
+ * the last range's end (the CHECK at KVApp.h:544).  Returns once the bounds
+ * are known: the bound kernels write them, tagged, straight into pinned host
+ * memory, so a request costs no copy launch and no stream synchronisation
+ * (with lens, the per-slice sums still come back by a copy and a sync). */
 int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_vals,
               int num_servers, const uint64_t* begins_host,
               const uint64_t* ends_host, uint64_t* key_pos_host,

@@ -11,6 +11,8 @@
 // 24 dependent loads.  With lens, the value bound of each slice is a per-slice
 // sum of lens (KVApp.h:565-569), done as a 2-D grid of chunk partial sums.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <vector>
@@ -24,8 +26,15 @@ struct Targets {
   uint64_t v[kMaxTargets];
 };
 
+// pos_sys (may be NULL): the same bound into pinned host memory, tagged —
+// bits [0, 40) the position, [40, 64) the request's tag — as ONE system-scope
+// store per bound, so the host reads each bound as soon as its word carries
+// the tag: no copy launch, no stream synchronisation, and no ordering between
+// words to rely on (each word validates itself).
+constexpr int kPosBits = 40;
 __global__ __launch_bounds__(256) void k_bounds(const uint64_t* __restrict__ keys, uint64_t n,
-                                                Targets t, uint64_t* __restrict__ pos) {
+                                                Targets t, uint64_t* __restrict__ pos,
+                                                uint64_t* __restrict__ pos_sys, uint64_t tag) {
   const uint64_t target = t.v[blockIdx.x];
   uint64_t lo = 0, hi = n;  // the answer (first index with keys >= target) is in [lo, hi]
   while (hi - lo > (uint64_t)kBlock) {
@@ -45,7 +54,12 @@ __global__ __launch_bounds__(256) void k_bounds(const uint64_t* __restrict__ key
   const uint64_t p = lo + threadIdx.x;
   const int pred = (p < hi) && (keys[p] < target);
   const uint64_t c = (uint64_t)__syncthreads_count(pred);
-  if (threadIdx.x == 0) pos[blockIdx.x] = lo + c;
+  if (threadIdx.x == 0) {
+    pos[blockIdx.x] = lo + c;
+    if (pos_sys)
+      __hip_atomic_store(pos_sys + blockIdx.x, (lo + c) | (tag << kPosBits), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 constexpr uint64_t kLenChunk = 16384;  // lens per block
@@ -102,6 +116,9 @@ struct SliceScratch {
   uint64_t* pos_dev = nullptr;
   unsigned long long* sums_dev = nullptr;
   uint64_t* pos_host = nullptr;
+  uint64_t* pos_map = nullptr;      // tagged bounds, pinned + mapped (k_bounds' pos_sys)
+  uint64_t* pos_map_dev = nullptr;
+  uint64_t tag = 0;
   int cap = 0;
 };
 static thread_local std::map<int, SliceScratch> t_slice_scratch;
@@ -114,11 +131,17 @@ static int get_slice_scratch(int nb, SliceScratch** out) {
     if (s.pos_dev) (void)hipFree(s.pos_dev);
     if (s.sums_dev) (void)hipFree(s.sums_dev);
     if (s.pos_host) (void)hipHostFree(s.pos_host);
+    if (s.pos_map) (void)hipHostFree(s.pos_map);
+    const uint64_t tag = s.tag;
     s = SliceScratch();
+    s.tag = tag;
     const int cap = std::max(nb, 64);
     PSG_HIP(hipMalloc((void**)&s.pos_dev, cap * sizeof(uint64_t)));
     PSG_HIP(hipMalloc((void**)&s.sums_dev, cap * sizeof(unsigned long long)));
     PSG_HIP(hipHostMalloc((void**)&s.pos_host, cap * sizeof(uint64_t), hipHostMallocDefault));
+    PSG_HIP(hipHostMalloc((void**)&s.pos_map, cap * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+    PSG_HIP(hipHostGetDevicePointer((void**)&s.pos_map_dev, s.pos_map, 0));
+    memset(s.pos_map, 0, cap * sizeof(uint64_t));
     s.cap = cap;
   }
   *out = &s;
@@ -171,6 +194,12 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
   uint64_t* pos_dev = sc->pos_dev;
   unsigned long long* sums_dev = sc->sums_dev;
   int rc = PSG_OK;
+  // the bounds come back tagged through pinned memory (k_bounds' pos_sys),
+  // read as soon as every word carries this request's tag; n < 2^40 keys
+  const bool tagged = n < (1ull << kPosBits);
+  sc->tag = (sc->tag + 1) & ((1ull << (64 - kPosBits)) - 1);
+  if (sc->tag == 0) sc->tag = 1;
+  const uint64_t tag = sc->tag;
   for (int b0 = 0; b0 < nb; b0 += kMaxTargets) {
     Targets t;
     const int cnt = std::min(kMaxTargets, nb - b0);
@@ -178,12 +207,32 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
       const int b = b0 + j;
       t.v[j] = b == 0 ? begins_host[0] : ends_host[b - 1];
     }
-    k_bounds<<<cnt, kBlock, 0, st>>>(keys, n, t, pos_dev + b0);
+    k_bounds<<<cnt, kBlock, 0, st>>>(keys, n, t, pos_dev + b0, tagged ? sc->pos_map_dev + b0 : nullptr, tag);
   }
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpyAsync(sc->pos_host, pos_dev, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e == hipSuccess) memcpy(key_pos_host, sc->pos_host, nb * sizeof(uint64_t));
+  bool got = false;
+  if (e == hipSuccess && tagged) {
+    // spin for ~2 ms at most (then the stream sync below reports any fault)
+    const volatile uint64_t* w = sc->pos_map;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; !got; ++spin) {
+      int b = 0;
+      while (b < nb && (w[b] >> kPosBits) == tag) ++b;
+      if (b == nb) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        for (int i = 0; i < nb; ++i) key_pos_host[i] = w[i] & ((1ull << kPosBits) - 1);
+        got = true;
+        break;
+      }
+      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  if (e == hipSuccess && !got) {
+    e = hipMemcpyAsync(sc->pos_host, pos_dev, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) memcpy(key_pos_host, sc->pos_host, nb * sizeof(uint64_t));
+  }
   if (e != hipSuccess) {
     rc = hip_fail(e, "psg_slice bounds", __FILE__, __LINE__);
   } else if (key_pos_host[num_servers] != n) {

@@ -187,3 +187,60 @@ def test_lr_apply_matches_reference_formula():
 def test_cpu_baseline_runs():
     first, push, pull = oracle.bench(20000, 2)
     assert first > 0 and push > 0 and pull > 0
+
+
+@pytest.mark.parametrize("dtype", [oracle.F32, oracle.F64, oracle.F16, oracle.BF16])
+def test_out_of_order_and_repeated_keys_follow_the_sequential_loop(dtype):
+    """oracle.Store on requests with keys in any order and repeated — the
+    semantics the GPU's order-preserving path is checked against — equals a
+    pure-Python replay of KVApp.h:446-454 (`store[key] += vals[i]` per
+    occurrence, a PushPull answering the running value), addition by addition
+    in the element type (f16 / bf16: each sum rounded once from f32, RNE)."""
+    rng = np.random.default_rng(3 + dtype)
+    keys = rng.integers(0, 50, 400).astype(np.uint64)
+    vals = oracle.synth(400, dtype, 11, 1, -1.0, 1.0)
+    np_t = {oracle.F32: np.float32, oracle.F64: np.float64}.get(dtype)
+
+    def add(a, b):
+        if np_t is not None:
+            return np_t(np_t(a) + np_t(b))
+        # f16 / bf16 bits: widen to f32, add, round once to the 16-bit type
+        fa, fb = _half_to_f32(a, dtype), _half_to_f32(b, dtype)
+        return _f32_to_half(np.float32(fa + fb), dtype)
+
+    zero = np_t(0) if np_t is not None else np.uint16(0)
+    ref, outs = {}, []
+    for flags in (oracle.PUSH, oracle.PUSH | oracle.PULL, oracle.PULL):
+        o = []
+        for k, v in zip(keys.tolist(), vals):
+            if flags & oracle.PUSH:
+                ref[k] = add(ref.get(k, zero), v)
+            if flags & oracle.PULL:
+                o.append(ref.setdefault(k, zero))
+        outs.append(np.array(o))
+    st = oracle.Store(dtype)
+    got = [st.handle(f, keys, vals if f & oracle.PUSH else None, 400)
+           for f in (oracle.PUSH, oracle.PUSH | oracle.PULL, oracle.PULL)]
+    np.testing.assert_array_equal(got[1], outs[1].astype(got[1].dtype))
+    np.testing.assert_array_equal(got[2], outs[2].astype(got[2].dtype))
+    k, v = st.dump()
+    assert sorted(k.tolist()) == sorted(ref)
+    exp = np.array([ref[int(x)] for x in k]).astype(v.dtype)
+    np.testing.assert_array_equal(v, exp)
+
+
+def _half_to_f32(bits, dtype):
+    b = np.uint16(bits)
+    if dtype == oracle.F16:
+        return np.float32(b.view(np.float16))
+    return np.array([np.uint32(b) << np.uint32(16)], np.uint32).view(np.float32)[0]
+
+
+def _f32_to_half(x, dtype):
+    if dtype == oracle.F16:
+        return np.float16(x).view(np.uint16)
+    u = int(np.array([x], np.float32).view(np.uint32)[0])
+    if (u & 0x7F800000) == 0x7F800000 and (u & 0x7FFFFF):  # NaN
+        return np.uint16((u >> 16) | 0x40)
+    r = u + 0x7FFF + ((u >> 16) & 1)  # round to nearest even
+    return np.uint16((r >> 16) & 0xFFFF)

@@ -12,6 +12,8 @@
 #                                                      key-cached Push (two passes each)
 #   trace    kernel trace of the keyed bench: durations and the idle gaps between
 #            launches (tools/trace_gaps.py)
+#   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
+#            (tools/pmc_targets.py, two passes each)
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -43,6 +45,13 @@ for st in "$@"; do
           step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
           step 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_w_$st.log 2>&1; echo "$st write rc=$?"
           python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" 10000000 gpurun_out/$out $per ;;
+    pmcpull|pmcadam)
+          if [ "$st" = pmcpull ]; then tg=pull256; ks="k_dense_vec<0, 2,"; keys=268435456; per=8; out=pmc_pull256_traffic.json
+          else tg=adam64; ks="k_lr_apply_sum<true"; keys=67108864; per=56; out=pmc_lr_adam64_traffic.json; fi
+          rm -rf gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st
+          step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 tools/pmc_targets.py $tg > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
+          step 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w_$st -- python3 tools/pmc_targets.py $tg > gpurun_out/pmc_w_$st.log 2>&1; echo "$st write rc=$?"
+          python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" $keys gpurun_out/$out $per; cat gpurun_out/$out ;;
     trace) rm -rf gpurun_out/trace_keyed
           step 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_keyed -o run -- python3 bench.py --workload keyed --no-cpu-baseline --no-probe256 --steps 10 --warmup 2 > gpurun_out/trace_keyed.json 2>&1; echo "trace rc=$?"
           python3 tools/trace_gaps.py gpurun_out/trace_keyed/run_kernel_trace.csv 8 ;;
