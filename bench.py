@@ -804,8 +804,10 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
                                    "SORTED-store Push: k_validate_windows + k_resolve_apply "
                                    "(whole-request validation before any write; tile windows "
-                                   "cached per key array; completion word written by the "
-                                   "kernel; one server, so no slicer pass)", vb)
+                                   "cached per key array; requests in flight, each reporting "
+                                   "completion and flags in one kernel-written word; one "
+                                   "server, so no slicer pass)", vb)
+        res["pull_roofline_frac"] = round(24 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
                                    "k_dense_vec<PUSH> (store += vals)", vb)
