@@ -412,6 +412,10 @@ class GpuBackend:
             if self.mode.startswith("xgmi-keyed"):
                 self._calibrate_keyed(iters)
             return
+        first = 0
+        if self.comm is not None:
+            self._first_collective()
+            first = 1  # one Push (and Pull) outside the timing
         cands = [("rccl", 1), ("rccl", 4), ("rccl", 8), ("rccl", 16)] if self.comm is not None else []
         two_stream = [("xgmi", 2), ("xgmi", 4), ("xgmiw", 2), ("xgmiw", 4)]
         if self.xgmi is not None:
@@ -447,7 +451,7 @@ class GpuBackend:
         self._set_mode(cands[order[0]])
         self.calibration = {f"{m}{'' if nb == 0 else '/' + str(nb)}": round(x, 4)
                             for (m, nb), x in zip(cands, t)}
-        self.pushes_in_calibration = len(cands) * (iters + 1)
+        self.pushes_in_calibration = len(cands) * (iters + 1) + first
         if self.mode in ("xgmi", "xgmiw"):
             self.pushes_in_calibration += 1
             self.exchange_verified = self._verify_xgmi()
@@ -459,6 +463,25 @@ class GpuBackend:
                 print("xGMI exchange failed its checksum verification; using RCCL",
                       file=sys.stderr)
                 self._set_mode(rest[0])
+
+    def _first_collective(self):
+        """The first RCCL step (it also sets up the peer connections) waited for
+        against PSG_COMM_TIMEOUT_S (psg_comm_sync): if it does not complete on
+        every rank, every rank aborts its communicators and the exchange is the
+        xGMI kernels alone — a transport that never connects ends in a fallback,
+        not a hang."""
+        ok = True
+        self._set_mode(("rccl", 1))
+        try:
+            self._one_step()
+            self.comm.sync(self.stream)
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {self.rank}: first RCCL step failed ({e})", file=sys.stderr)
+            ok = False
+        if not all(self.group.all_gather(ok)):
+            self.comm.abort()
+            self.comm = None
+            self.first_collective_failed = True
 
     def _calibrate_keyed(self, iters):
         """The key-cached xGMI exchange: the read-form Pull (psg_xgmi_pull_slots)
@@ -791,6 +814,9 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
             res["config"]["exchange"] = ("RCCL pipelined reduce/broadcast, %d buckets" % backend.nbuckets
                                          if fused else "RCCL reduce-scatter then all-gather")
         res["config"]["calibration_ms"] = getattr(backend, "calibration", None)
+        if getattr(backend, "first_collective_failed", False):
+            res["config"]["rccl"] = ("aborted on every rank: the first collective did not complete within "
+                                     "PSG_COMM_TIMEOUT_S (psg_comm_sync); xGMI kernels only")
         if hasattr(backend, "exchange_verified"):
             res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
         if getattr(backend, "share_gpu", False):

@@ -311,6 +311,15 @@ int psg_comm_bucket_plan(uint64_t blk, int nbuckets, uint64_t* offs, uint64_t* c
 int psg_comm_keyed_plan(const uint64_t* key_pos_host, int nranks, uint64_t n, uint64_t* maxseg);
 int psg_comm_destroy(psg_comm* c);
 int psg_comm_rank(psg_comm* c, int* rank, int* nranks);
+/* Wait for the collectives queued on `stream` (and the comm's side stream) for
+ * at most timeout_s (<= 0: PSG_COMM_TIMEOUT_S).  On a timeout the communicators
+ * are aborted (their kernels leave their wait loops), every later collective
+ * call on c fails with PSG_ERR_COMM, and so does this one: a caller that runs
+ * a first collective under it can fall back instead of hanging. */
+int psg_comm_sync(psg_comm* c, psg_stream stream, double timeout_s);
+/* Abort the communicators now (every rank of a job that gives up on RCCL
+ * together calls it); later collective calls on c fail with PSG_ERR_COMM. */
+int psg_comm_abort(psg_comm* c);
 
 /* BSP Push of a dense vector: every rank contributes its worker's full vector
  * vals[n_total]; rank r's DENSE store `shard` owns the contiguous block

@@ -36,6 +36,7 @@ struct psg_comm {
   hipStream_t side;
   std::vector<hipEvent_t> ev;  // per-bucket "accumulated" events
   hipEvent_t side_done;
+  bool aborted;  // psg_comm_sync timed out and aborted the communicators
 };
 
 namespace psg {
@@ -63,6 +64,7 @@ static bool nccl_type(int dtype, ncclDataType_t* t) {
 
 static int check_shard(psg_comm* c, psg_store* s, uint64_t n_total, uint64_t* blk) {
   PSG_REQUIRE(c && s, PSG_ERR_INVALID, "psg_comm: null comm or store");
+  PSG_REQUIRE(!c->aborted, PSG_ERR_COMM, "psg_comm: the communicators were aborted (psg_comm_sync timed out)");
   PSG_REQUIRE(s->kind == PSG_STORE_DENSE, PSG_ERR_INVALID, "psg_comm: shard must be a DENSE store");
   PSG_REQUIRE(n_total % (uint64_t)c->nranks == 0, PSG_ERR_INVALID,
               "psg_comm: n_total %llu not divisible by %d ranks", (unsigned long long)n_total,
@@ -208,6 +210,43 @@ int psg_comm_destroy(psg_comm* c) {
   for (int k = 0; k < 2; ++k)
     if (c->comm[k]) ncclCommDestroy(c->comm[k]);
   delete c;
+  return PSG_OK;
+}
+
+int psg_comm_sync(psg_comm* c, psg_stream stream, double timeout_s) {
+  PSG_REQUIRE(c, PSG_ERR_INVALID, "psg_comm_sync: null comm");
+  PSG_REQUIRE(!c->aborted, PSG_ERR_COMM, "psg_comm_sync: the communicators were aborted");
+  const auto deadline = std::chrono::steady_clock::now() +
+                        std::chrono::microseconds((int64_t)((timeout_s > 0 ? timeout_s : comm_timeout_s()) * 1e6));
+  hipStream_t sts[2] = {(hipStream_t)stream, c->side};
+  for (hipStream_t st : sts) {
+    for (;;) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return hip_fail(q, "psg_comm_sync", __FILE__, __LINE__);
+      if (std::chrono::steady_clock::now() > deadline) {
+        // a collective that cannot complete (a peer gone, a transport that
+        // never connected): abort the communicators, whose kernels then leave
+        // their wait loops, and report it instead of hanging
+        for (int k = 0; k < kCommIds; ++k)
+          if (c->comm[k]) (void)ncclCommAbort(c->comm[k]);
+        for (int k = 0; k < kCommIds; ++k) c->comm[k] = nullptr;
+        c->aborted = true;
+        set_error("psg_comm_sync: the collectives did not complete within %.0f s; communicators aborted", timeout_s);
+        return PSG_ERR_COMM;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+  }
+  return PSG_OK;
+}
+
+int psg_comm_abort(psg_comm* c) {
+  PSG_REQUIRE(c, PSG_ERR_INVALID, "psg_comm_abort: null comm");
+  for (int k = 0; k < kCommIds; ++k)
+    if (c->comm[k]) (void)ncclCommAbort(c->comm[k]);
+  for (int k = 0; k < kCommIds; ++k) c->comm[k] = nullptr;
+  c->aborted = true;
   return PSG_OK;
 }
 
@@ -373,6 +412,7 @@ int psg_comm_keyed_plan(const uint64_t* kp, int nranks, uint64_t n, uint64_t* ma
 static int keyed_args(psg_comm* c, psg_store* s, const uint64_t* keys, uint64_t n,
                       const uint64_t* kp, uint64_t* maxseg) {
   PSG_REQUIRE(c && s && kp, PSG_ERR_INVALID, "psg_comm keyed: null argument");
+  PSG_REQUIRE(!c->aborted, PSG_ERR_COMM, "psg_comm: the communicators were aborted (psg_comm_sync timed out)");
   PSG_REQUIRE(n == 0 || keys, PSG_ERR_INVALID, "psg_comm keyed: null keys");
   return psg_comm_keyed_plan(kp, c->nranks, n, maxseg);
 }

@@ -46,7 +46,7 @@ EXPORTS = [
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
-    "psg_comm_bucket_plan", "psg_comm_keyed_plan",
+    "psg_comm_bucket_plan", "psg_comm_keyed_plan", "psg_comm_sync", "psg_comm_abort",
     "psg_adam_create", "psg_adam_destroy", "psg_lr_apply", "psg_lr_apply_sum",
     "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
@@ -123,6 +123,7 @@ def lib() -> C.CDLL:
             "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
             "psg_comm_id_bytes": ([], i32), "psg_comm_get_id": ([vp], i32),
             "psg_comm_bucket_plan": ([u64, i32, vp, vp, i32, C.POINTER(i32)], i32),
+            "psg_comm_sync": ([vp, vp, f64], i32), "psg_comm_abort": ([vp], i32),
             "psg_comm_keyed_plan": ([vp, i32, u64, C.POINTER(u64)], i32),
             "psg_comm_init": ([vp, i32, i32, C.POINTER(vp)], i32),
             "psg_comm_destroy": ([vp], i32),
@@ -458,6 +459,13 @@ class Comm:
         self.h = C.c_void_p(None)
         buf = C.create_string_buffer(uid, len(uid))
         _call("psg_comm_init", buf, nranks, rank, C.byref(self.h))
+
+    def sync(self, stream=None, timeout_s: float = 0.0) -> None:
+        """Wait for the queued collectives, at most timeout_s; aborts them and raises on a timeout."""
+        _call("psg_comm_sync", self.h, _s(stream), timeout_s)
+
+    def abort(self) -> None:
+        _call("psg_comm_abort", self.h)
 
     def push(self, shard: Store, vals, n_total: int, scratch=None, stream=None) -> None:
         _call("psg_comm_push", self.h, shard.h, _ptr(vals), n_total, _ptr(scratch), _s(stream))

@@ -752,6 +752,26 @@ def test_comm_single_rank_push_pull(force, dtype, n, monkeypatch):
     c.close()
 
 
+def test_comm_sync_and_abort(monkeypatch):
+    """psg_comm_sync waits for the queued collectives against a deadline;
+    psg_comm_abort (what every rank calls when one rank's first collective did
+    not complete) makes every later collective fail with PSG_ERR_COMM."""
+    monkeypatch.setenv("PSG_COMM_FORCE_COLLECTIVE", "1")
+    c = psg.Comm(psg.comm_id(), 1, 0)
+    n = 1 << 16
+    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
+    v = dev(np.ones(n, np.float32))
+    s = psg.Stream()
+    c.push(st, v, n, stream=s)
+    c.sync(s, 30.0)
+    np.testing.assert_array_equal(st.dump()[1], np.ones(n, np.float32))
+    c.abort()
+    with pytest.raises(psg.PsgError) as ei:
+        c.push(st, v, n, stream=s)
+    assert ei.value.code == 5
+    c.close()
+
+
 _NEVER_JOINS = r"""
 import sys, time
 sys.path.insert(0, sys.argv[1])

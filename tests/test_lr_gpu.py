@@ -209,3 +209,30 @@ def test_xgmi_lr_push_multiprocess(world, adam):
         exp[s * blk:(s + 1) * blk] = replay(w0[s * blk:(s + 1) * blk].copy(), rs, adam)
     for r in range(world):
         np.testing.assert_array_equal(results[r], exp, err_msg=f"rank {r}'s pulled model")
+
+
+LRG = np.load(os.path.join(ROOT, "tests", "golden", "lr_ref.npz"))
+
+
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("case", [str(c) for c in LRG["cases"]])
+def test_lr_apply_matches_the_reference_adam(case, fused):
+    """psg_lr_apply (the merged frame) and psg_lr_apply_sum (the merge fused in)
+    against rounds computed by the REFERENCE's own Adam (tests/src/Adam.h,
+    compiled where it lies, inside LRServer's apply loop; fixture
+    tests/golden/make_lr_golden.py): bit for bit, round by round, SGD and Adam,
+    repeated and skipped iterations."""
+    w0 = LRG[f"{case}_w0"]
+    n = len(w0)
+    lr = float(LRG[f"{case}_lr"][0])
+    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
+    st.handle(psg.PUSH, None, dev(w0), None, n)
+    a = psg.Adam(n, lr) if LRG[f"{case}_adam"][0] else None
+    for r, it in enumerate(LRG[f"{case}_iters"]):
+        g = dev(LRG[f"{case}_merged"][r])
+        if fused:
+            psg.lr_apply_sum(st, [g], n, lr, a, int(it))
+        else:
+            psg.lr_apply(st, g, n, lr, a, int(it))
+        _, got = st.dump()
+        np.testing.assert_array_equal(got, LRG[f"{case}_out"][r], err_msg=f"{case} round {r}")

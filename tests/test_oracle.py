@@ -244,3 +244,23 @@ def _f32_to_half(x, dtype):
         return np.uint16((u >> 16) | 0x40)
     r = u + 0x7FFF + ((u >> 16) & 1)  # round to nearest even
     return np.uint16((r >> 16) & 0xFFFF)
+
+
+LRG = np.load(os.path.join(HERE, "golden", "lr_ref.npz"))
+
+
+@pytest.mark.parametrize("case", [str(c) for c in LRG["cases"]])
+def test_lr_apply_matches_the_reference_adam(case):
+    """oracle.lr_apply against LR rounds computed by the REFERENCE's own Adam
+    (tests/src/Adam.h compiled where it lies into oracle/_ref/ref_lr_driver,
+    run inside LRServer's apply loop, LRServer.h:171-177; fixture written by
+    tests/golden/make_lr_golden.py): bit for bit, round by round."""
+    w = LRG[f"{case}_w0"].copy()
+    lr = float(LRG[f"{case}_lr"][0])
+    adam = bool(LRG[f"{case}_adam"][0])
+    n = len(w)
+    m = np.zeros(n) if adam else None
+    v = np.zeros(n) if adam else None
+    for r, it in enumerate(LRG[f"{case}_iters"]):
+        oracle.lr_apply(w, LRG[f"{case}_merged"][r], lr, m, v, lr, 0.9, 0.999, 1e-8, int(it))
+        np.testing.assert_array_equal(w, LRG[f"{case}_out"][r], err_msg=f"{case} round {r}")
