@@ -296,6 +296,40 @@ def test_sorted_out_of_order_request_on_a_populated_store(bad, flags):
     np.testing.assert_array_equal(st.dump()[1], orc.dump()[1])
 
 
+@pytest.mark.parametrize("where", ["none", "tile_0", "tile_500", "last_tile"])
+def test_out_of_order_pushpull_at_scale(where):
+    """A 4 M-key PushPull (about a thousand 4096-key tiles) on a store holding
+    half the keys, with a pair out of order and a repeat in tile `where`: the
+    fast path's checks catch it wherever it sits and write nothing, and the
+    order-preserving path serves the whole request (inserting the absent keys)
+    — bit-exact against the oracle, replies and store, twice in a row."""
+    rng = np.random.default_rng(5)
+    univ = np.unique(rng.integers(0, KMAX, 4_200_000, dtype=np.uint64))[:4_000_000]
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    half = univ[::2].copy()
+    w = rng.uniform(-1, 1, len(half)).astype(np.float32)
+    st.handle(psg.PUSH, dev(half), dev(w), None, len(half))
+    orc.handle(oracle.PUSH, half, w, len(half))
+    k = univ.copy()
+    pos = {"none": None, "tile_0": 100, "tile_500": 500 * 4096 + 7, "last_tile": len(k) - 3}[where]
+    if pos is not None:
+        k[pos], k[pos + 1] = k[pos + 1], k[pos]
+        k[pos + 2] = k[pos - 5]  # and a repeat
+    n = len(k)
+    v = rng.uniform(-1, 1, n).astype(np.float32)
+    out = psg.DeviceBuffer(n * 4)
+    for _ in range(2):
+        st.handle(psg.PUSH | psg.PULL, dev(k), dev(v), out, n)
+        exp = orc.handle(oracle.PUSH | oracle.PULL, k, v, n)
+        np.testing.assert_array_equal(out.download(np.float32, n), exp)
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    o = np.argsort(ok)
+    np.testing.assert_array_equal(gk, ok[o])
+    np.testing.assert_array_equal(gv, ov[o])
+
+
 @pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL])
 def test_sorted_out_of_range_request_leaves_a_populated_store_unchanged(flags):
     """A key outside the shard's range rejects the request as a whole
