@@ -216,8 +216,12 @@ struct psg_store {
 struct psg_adam {
   uint64_t n;
   double lr, beta1, beta2, eps;
-  double* m;  // n doubles each (Adam.h:40-41), 16-B aligned (hipMalloc)
+  // the moments of Adam.h:40-41: blocked (default) — one array with, per 128
+  // features, their 128 m then their 128 v values (m; v unused) — or two
+  // arrays of n doubles (PSG_ADAM_BLOCKED=0); 16-B aligned (hipMalloc)
+  double* m;
   double* v;
+  int blocked;
 };
 
 namespace psg {

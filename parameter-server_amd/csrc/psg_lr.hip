@@ -47,9 +47,17 @@ __device__ __forceinline__ void st_nt(V* p, V x, int nt) {
   else *p = x;
 }
 
+// Adam moments, BLK layout (psg_adam.blocked): one array holding, per 128
+// features, their 128 m values then their 128 v values (2 KiB), so a wave's m
+// and v runs for the same features are neighbours in memory — one stream of
+// moment pairs instead of two.  Element accessors for feature i:
+__device__ __forceinline__ uint64_t blk_m(uint64_t i) { return (i >> 7) * 256 + (i & 127); }
+__device__ __forceinline__ uint64_t blk_v(uint64_t i) { return (i >> 7) * 256 + 128 + (i & 127); }
+
 // MAXG: gradient slots the kernel keeps registers for (4 when ng <= 4: 125 ->
-// fewer VGPRs, more waves in flight; else kMaxGrads).
-template <bool ADAM, bool ZERO, int MAXG>
+// fewer VGPRs, more waves in flight; else kMaxGrads).  BLK: the moments in the
+// blocked layout (m is the one array, v unused).
+template <bool ADAM, bool ZERO, int MAXG, bool BLK>
 __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Grads g, int ng, uint64_t n,
                                                       float lr, double* __restrict__ m,
                                                       double* __restrict__ v, double alr, double b1,
@@ -98,11 +106,25 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
                 f32x2, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g.p[k] + f0 + 128 * h)));
       f32x2 wv[2];
       f64x2 mm[2], vv[2];
+      // the moment pairs of features f0 + 128 h (BLK: group 2T + h of the
+      // blocked array, T = f0 / 256, at lane offset f0 % 128)
+      double* mp[2];
+      double* vp[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (BLK) {
+          mp[h] = m + blk_m(f0 + 128 * h);
+          vp[h] = m + blk_v(f0 + 128 * h);
+        } else {
+          mp[h] = m + f0 + 128 * h;
+          vp[h] = v + f0 + 128 * h;
+        }
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         wv[h] = __builtin_bit_cast(f32x2, ld_nt(reinterpret_cast<const u32x2*>(w + f0 + 128 * h), nt));
-        mm[h] = ld_nt(reinterpret_cast<const f64x2*>(m + f0 + 128 * h), nt);
-        vv[h] = ld_nt(reinterpret_cast<const f64x2*>(v + f0 + 128 * h), nt);
+        mm[h] = ld_nt(reinterpret_cast<const f64x2*>(mp[h]), nt);
+        vv[h] = ld_nt(reinterpret_cast<const f64x2*>(vp[h]), nt);
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -119,8 +141,8 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
           vv[h][e] = vi;
           wv[h][e] = (float)((double)wv[h][e] - alr * (mi / c1) / (sqrt(vi / c2) + eps));
         }
-        st_nt(reinterpret_cast<f64x2*>(m + f0 + 128 * h), mm[h], nt);
-        st_nt(reinterpret_cast<f64x2*>(v + f0 + 128 * h), vv[h], nt);
+        st_nt(reinterpret_cast<f64x2*>(mp[h]), mm[h], nt);
+        st_nt(reinterpret_cast<f64x2*>(vp[h]), vv[h], nt);
         st_nt(reinterpret_cast<u32x2*>(w + f0 + 128 * h), __builtin_bit_cast(u32x2, wv[h]), nt);
       }
     }
@@ -130,10 +152,12 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
     for (int k = 1; k < ng; ++k) s = s + g.p[k][i];
     double grad = (double)(lr * s);
     if constexpr (ADAM) {
-      const double mi = b1 * m[i] + (1.0 - b1) * grad;
-      const double vi = b2 * v[i] + (1.0 - b2) * grad * grad;
-      m[i] = mi;
-      v[i] = vi;
+      double* mi_p = BLK ? m + blk_m(i) : m + i;
+      double* vi_p = BLK ? m + blk_v(i) : v + i;
+      const double mi = b1 * *mi_p + (1.0 - b1) * grad;
+      const double vi = b2 * *vi_p + (1.0 - b2) * grad * grad;
+      *mi_p = mi;
+      *vi_p = vi;
       grad = alr * (mi / c1) / (sqrt(vi / c2) + eps);
     }
     w[i] = (float)((double)w[i] - grad);
@@ -165,9 +189,10 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   if (adam) {
     PSG_REQUIRE(adam_off <= adam->n && n <= adam->n - adam_off, PSG_ERR_RANGE,
                 "LR apply: Adam state holds %llu features", (unsigned long long)adam->n);
-    m = adam->m + adam_off;
-    v = adam->v + adam_off;
-    vec = vec && aligned16(m) && aligned16(v);
+    PSG_REQUIRE(!adam->blocked || adam_off == 0, PSG_ERR_INVALID, "LR apply: blocked Adam state at an offset");
+    m = adam->m + (adam->blocked ? 0 : adam_off);
+    v = adam->blocked ? nullptr : adam->v + adam_off;
+    vec = vec && aligned16(m) && (adam->blocked || aligned16(v));
     // the two bias corrections of Adam.h:31-32, with the host libm pow the
     // reference calls
     c1 = 1 - std::pow(adam->beta1, iteration + 1);
@@ -188,21 +213,32 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   const int ntm = nt_env >= 0 ? (nt_env ? 1 : 0) : (state_bytes > (512ull << 20) ? 1 : 0);
   const double alr = adam ? adam->lr : 0, b1 = adam ? adam->beta1 : 0, b2 = adam ? adam->beta2 : 0,
                eps = adam ? adam->eps : 0;
-#define PSG_LR_LAUNCH(A, Z, G)                                                                        \
-  k_lr_apply_sum<A, Z, G><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
+#define PSG_LR_LAUNCH(A, Z, G, B)                                                                     \
+  k_lr_apply_sum<A, Z, G, B><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
   const bool few = ngrads <= 4;
+  const bool blk = adam && adam->blocked;
   if (adam && from_zero) {
-    if (few) PSG_LR_LAUNCH(true, true, 4);
-    else PSG_LR_LAUNCH(true, true, kMaxGrads);
+    if (blk) {
+      if (few) PSG_LR_LAUNCH(true, true, 4, true);
+      else PSG_LR_LAUNCH(true, true, kMaxGrads, true);
+    } else {
+      if (few) PSG_LR_LAUNCH(true, true, 4, false);
+      else PSG_LR_LAUNCH(true, true, kMaxGrads, false);
+    }
   } else if (adam) {
-    if (few) PSG_LR_LAUNCH(true, false, 4);
-    else PSG_LR_LAUNCH(true, false, kMaxGrads);
+    if (blk) {
+      if (few) PSG_LR_LAUNCH(true, false, 4, true);
+      else PSG_LR_LAUNCH(true, false, kMaxGrads, true);
+    } else {
+      if (few) PSG_LR_LAUNCH(true, false, 4, false);
+      else PSG_LR_LAUNCH(true, false, kMaxGrads, false);
+    }
   } else if (from_zero) {
-    if (few) PSG_LR_LAUNCH(false, true, 4);
-    else PSG_LR_LAUNCH(false, true, kMaxGrads);
+    if (few) PSG_LR_LAUNCH(false, true, 4, false);
+    else PSG_LR_LAUNCH(false, true, kMaxGrads, false);
   } else {
-    if (few) PSG_LR_LAUNCH(false, false, 4);
-    else PSG_LR_LAUNCH(false, false, kMaxGrads);
+    if (few) PSG_LR_LAUNCH(false, false, 4, false);
+    else PSG_LR_LAUNCH(false, false, kMaxGrads, false);
   }
 #undef PSG_LR_LAUNCH
   PSG_HIP(hipGetLastError());
@@ -226,10 +262,23 @@ int psg_adam_create(uint64_t n, double learning_rate, double beta1, double beta2
   a->beta1 = beta1;
   a->beta2 = beta2;
   a->eps = epsilon;
-  hipError_t e = hipMalloc((void**)&a->m, n * sizeof(double));
-  if (e == hipSuccess) e = hipMalloc((void**)&a->v, n * sizeof(double));
-  if (e == hipSuccess) e = hipMemset(a->m, 0, n * sizeof(double));
-  if (e == hipSuccess) e = hipMemset(a->v, 0, n * sizeof(double));
+  // PSG_ADAM_BLOCKED=0: m and v as two arrays (A/B); default the blocked layout
+  static const int blocked = [] {
+    const char* e = getenv("PSG_ADAM_BLOCKED");
+    return e ? (atoi(e) != 0) : 1;
+  }();
+  a->blocked = blocked;
+  hipError_t e;
+  if (blocked) {
+    const uint64_t words = (n + 127) / 128 * 256;
+    e = hipMalloc((void**)&a->m, words * sizeof(double));
+    if (e == hipSuccess) e = hipMemset(a->m, 0, words * sizeof(double));
+  } else {
+    e = hipMalloc((void**)&a->m, n * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&a->v, n * sizeof(double));
+    if (e == hipSuccess) e = hipMemset(a->m, 0, n * sizeof(double));
+    if (e == hipSuccess) e = hipMemset(a->v, 0, n * sizeof(double));
+  }
   if (e != hipSuccess) {
     psg_adam_destroy(a);
     return hip_fail(e, "psg_adam_create", __FILE__, __LINE__);
