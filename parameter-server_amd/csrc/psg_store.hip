@@ -357,44 +357,54 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
     }
     return;
   }
-  // 8 consecutive keys per lane (four 16-B loads in flight); the key before a
-  // lane's eight is the previous lane's last, handed over by a shuffle — only
-  // lane 0 of a wave loads it.  The loop bound is block-uniform (the shuffle
-  // needs every lane).
-  constexpr int kV = 8;
+  // Each wave checks 512 consecutive keys as 4 rows of 128: row h's load is
+  // one contiguous KiB (lane l holds keys 2l, 2l+1 of the row, one 16-B
+  // load), and the 4 loads are in flight together.  The key before a lane's
+  // pair is the previous lane's second (a shuffle), the previous row's last
+  // (lane 63's, broadcast) for lane 0, and for row 0 the key before the
+  // wave's run, which lane 0 loads.  The loop bound is block-uniform (the
+  // shuffles need every lane).
+  constexpr int kRows = 4, kRowKeys = 128, kWaveKeys = kRows * kRowKeys;
   int range = 0, unsorted = 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t nvb = (uint64_t)gridDim.x - nsearch;
-  for (uint64_t base = (uint64_t)(blockIdx.x - nsearch) * kBlock * kV; base < n;
-       base += nvb * kBlock * kV) {
-    const uint64_t i0 = base + (uint64_t)threadIdx.x * kV;
-    uint64_t key[kV];
-    if (i0 + kV <= n && vec) {
+  constexpr uint64_t kBlockKeys = (uint64_t)(kBlock / 64) * kWaveKeys;  // 2048
+  for (uint64_t base = (uint64_t)(blockIdx.x - nsearch) * kBlockKeys; base < n; base += nvb * kBlockKeys) {
+    const uint64_t wbase = base + (uint64_t)wv * kWaveKeys;
+    uint64_t k0[kRows], k1[kRows];
 #pragma unroll
-      for (int h = 0; h < kV / 2; ++h) {
-        const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0 + 2 * h);
-        key[2 * h] = a[0];
-        key[2 * h + 1] = a[1];
+    for (int h = 0; h < kRows; ++h) {
+      const uint64_t i = wbase + (uint64_t)h * kRowKeys + 2 * (uint64_t)lane;
+      if (i + 2 <= n && vec) {
+        const u64x2 a = *reinterpret_cast<const u64x2*>(q + i);
+        k0[h] = a[0];
+        k1[h] = a[1];
+      } else {
+        k0[h] = i < n ? q[i] : 0;
+        k1[h] = i + 1 < n ? q[i + 1] : 0;
       }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kV; ++k) key[k] = i0 + k < n ? q[i0 + k] : 0;
     }
-    uint64_t last = key[kV - 1];
-    if (i0 + kV > n) last = i0 < n ? key[n - 1 - i0 < kV ? n - 1 - i0 : 0] : 0;
-    const uint32_t lo = __shfl_up((uint32_t)last, 1, 64), hi = __shfl_up((uint32_t)(last >> 32), 1, 64);
-    uint64_t prev = ((uint64_t)hi << 32) | lo;
-    bool have_prev = i0 < n;
-    if ((threadIdx.x & 63) == 0) {
-      have_prev = i0 > 0 && i0 < n;
-      prev = have_prev ? q[i0 - 1] : 0;
-    }
+    uint64_t before = 0;  // the key before the wave's run (lane 0)
+    if (lane == 0 && wbase > 0 && wbase < n) before = q[wbase - 1];
 #pragma unroll
-    for (int k = 0; k < kV; ++k) {
-      if (i0 + k < n) {
-        if (key[k] < kb || key[k] >= ke) range = 1;
-        if (have_prev && prev >= key[k]) unsorted = 1;
-        prev = key[k];
-        have_prev = true;
+    for (int h = 0; h < kRows; ++h) {
+      const uint64_t i = wbase + (uint64_t)h * kRowKeys + 2 * (uint64_t)lane;
+      const uint32_t plo = __shfl_up((uint32_t)k1[h], 1, 64), phi = __shfl_up((uint32_t)(k1[h] >> 32), 1, 64);
+      uint64_t prev = ((uint64_t)phi << 32) | plo;
+      uint64_t row_before = before;  // (h is unrolled: every lane runs the broadcast)
+      if (h > 0) {
+        const uint32_t llo = __shfl((uint32_t)k1[h - 1], 63, 64), lhi = __shfl((uint32_t)(k1[h - 1] >> 32), 63, 64);
+        row_before = ((uint64_t)lhi << 32) | llo;
+      }
+      if (lane == 0) prev = row_before;
+      const bool has_prev = i > 0 && i < n;
+      if (i < n) {
+        if (k0[h] < kb || k0[h] >= ke) range = 1;
+        if (has_prev && prev >= k0[h]) unsorted = 1;
+      }
+      if (i + 1 < n) {
+        if (k1[h] < kb || k1[h] >= ke) range = 1;
+        if (k0[h] >= k1[h]) unsorted = 1;
       }
     }
   }
