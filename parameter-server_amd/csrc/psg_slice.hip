@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <vector>
@@ -196,7 +197,11 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
   int rc = PSG_OK;
   // the bounds come back tagged through pinned memory (k_bounds' pos_sys),
   // read as soon as every word carries this request's tag; n < 2^40 keys
-  const bool tagged = n < (1ull << kPosBits);
+  static const bool poll_on = [] {  // PSG_SLICE_POLL=0: a copy + stream sync instead (A/B)
+    const char* e = getenv("PSG_SLICE_POLL");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool tagged = poll_on && n < (1ull << kPosBits);
   sc->tag = (sc->tag + 1) & ((1ull << (64 - kPosBits)) - 1);
   if (sc->tag == 0) sc->tag = 1;
   const uint64_t tag = sc->tag;
