@@ -183,11 +183,14 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * (PSG_ERR_RANGE) and leaves the store unchanged; out is then unspecified.
  * vals/out are device arrays of n elements of the store's dtype.
  * A keyed request (SORTED store, or DENSE with keys) returns once the request
- * is complete and its keys and vals are no longer read — the caller may reuse
- * them — while its last store and reply writes may still be in flight: work
- * that reads out or the store must be ordered after it on `stream`.  (On the
- * steady SORTED path it waits for the completion word its own kernel writes,
- * which also carries the request's flags, not for the stream.)  The store
+ * is complete: its keys and vals are no longer read — the caller may reuse
+ * them — and a Pull's reply is in memory, readable by any agent (a copy
+ * engine, the host, another stream) without synchronising `stream`.  Its last
+ * store writes may still be in flight: work that reads the store must be
+ * ordered after it on `stream`.  (On the steady SORTED path it waits for the
+ * completion word its own kernel writes, which also carries the request's
+ * flags, and for a Pull for a pinned word the stream writes behind the kernel
+ * — not for the stream itself.)  The store
  * remembers the LDS windows of the last few key arrays it saw (by device
  * pointer and n) and verifies them per tile, so a caller may rewrite a key
  * array in place between requests. */
@@ -205,7 +208,10 @@ int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,
  * write nothing; the wait that reaps it inserts the keys, clears the word and
  * replays those requests, in order — the store sees exactly the call sequence.
  * psg_store_wait(s, t) completes every request up to ticket t (0: all) and
- * returns the first failure of those not reported yet.  Every other store call
+ * returns the first failure of those not reported yet; when it returns, the
+ * replies of the Pulls reaped so far are in memory (it synchronises their
+ * stream once, rather than each request waiting for its own).  Every other
+ * store call
  * completes the requests in flight first. */
 int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys,
                            uint64_t first_key, const void* vals, void* out, uint64_t n,

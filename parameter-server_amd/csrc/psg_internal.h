@@ -148,6 +148,8 @@ struct InflightReq {
   uint32_t tag;   // the 24-bit tag that word will carry
   int wc;         // window-cache entry it ran on
   hipStream_t stream;
+  int want_land;  // a Pull answered when reaped (psg_store_handle): its reply must be in memory then
+  int land;       // ... and the stream writes tag to ring_host[kRing + ring] after the kernel to say so
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
 }  // namespace psg
@@ -185,6 +187,7 @@ struct psg_store {
   // kernel with one system-scope store (pinned host memory, kRing words)
   uint32_t* ring_host;
   uint32_t* ring_dev;
+  hipStream_t unlanded;  // a stream whose reaped async Pulls psg_store_wait still synchronises
   uint32_t ring_next;
   uint32_t tag;
   // fused requests in flight, in launch (= stream) order

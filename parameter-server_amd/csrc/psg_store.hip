@@ -1332,7 +1332,7 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
 
 template <int DT>
 static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals, void* out,
-                        hipStream_t st, InflightReq* rec) {
+                        hipStream_t st, InflightReq* rec, bool want_land) {
   const int nt = ra_block();
   const uint64_t tile = (uint64_t)nt * kPerLane;
   const uint64_t ntiles = (n + tile - 1) / tile;
@@ -1386,12 +1386,31 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     default: launch_apply<DT, PSG_PUSH | PSG_PULL>(s, q, n, vals, out, win, *rec, st); break;
   }
   PSG_HIP(hipGetLastError());
+  // a synchronous Pull's reply is read by whoever the caller answers (a copy
+  // engine, the host, another stream): behind the kernel the stream writes the
+  // tag into a pinned word, which lands after the kernel's end-of-kernel cache
+  // write-back, so seeing it means the reply is in memory — a poll instead of
+  // a stream synchronisation (PSG_PULL_LAND=0: the synchronisation, A/B).  A
+  // request in flight skips it: the write between two kernels costs ~7 us of
+  // a back-to-back stream, so psg_store_wait synchronises once instead.
+  static const int land_on = [] {
+    const char* e = getenv("PSG_PULL_LAND");
+    return e ? atoi(e) : 1;
+  }();
+  rec->want_land = want_land && (op & PSG_PULL);
+  rec->land = 0;
+  if (rec->want_land && land_on && sync_poll()) {
+    if (hipStreamWriteValue32(st, s->ring_dev + kRing + rec->ring, rec->tag, 0) == hipSuccess) rec->land = 1;
+    else (void)hipGetLastError();
+  }
   return PSG_OK;
 }
 
 // Wait for a fused request's completion word; after 2 ms (a long request, or a
 // fault) synchronise the stream, which also reports any error.
 // PSG_SYNC_POLL=0 always synchronises the stream first (A/B).
+static int wait_landed(psg_store* s, const InflightReq& r);
+
 static int wait_word(psg_store* s, const InflightReq& r, uint32_t* flags) {
   const volatile uint32_t* w = s->ring_host + r.ring;
   bool synced = false;
@@ -1418,6 +1437,31 @@ static int wait_word(psg_store* s, const InflightReq& r, uint32_t* flags) {
   return PSG_ERR_HIP;
 }
 
+// A Pull's reply in memory: its landed word (launch_fused), else the stream
+// synchronised.  Called once the request needs no follow-up (the follow-ups
+// end with a synchronisation of their own).
+static int wait_landed(psg_store* s, const InflightReq& r) {
+  if (!(r.op & PSG_PULL)) return PSG_OK;
+  if (!r.want_land) {  // in flight: psg_store_wait synchronises its stream
+    s->unlanded = r.stream;
+    return PSG_OK;
+  }
+  if (r.land) {
+    const volatile uint32_t* w = s->ring_host + kRing + r.ring;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      if (*w == r.tag) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return PSG_OK;
+      }
+      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  PSG_HIP(hipStreamSynchronize(r.stream));
+  return PSG_OK;
+}
+
 // After a fused request's word: the window-cache policy, then what the word
 // asks of the host.  A key outside the shard rejects the request (nothing was
 // written); keys out of order or repeated take the order-preserving path (the
@@ -1438,7 +1482,7 @@ static int finish(psg_store* s, const InflightReq& r, uint32_t f) {
     PSG_REQUIRE(false, PSG_ERR_RANGE, "request key outside the store range [%llu, %llu) (nothing applied)",
                 (unsigned long long)s->key_begin, (unsigned long long)s->key_end);
   if (f & W_UNSORTED) return general_request<DT>(s, r.op, r.q, r.vals, r.out, r.n, r.stream);
-  if (!(f & W_MISSING)) return PSG_OK;
+  if (!(f & W_MISSING)) return wait_landed(s, r);
   // the fused pass kept no slots: resolve again (the keys have not changed)
   // so the insert and the fixup know which keys were absent
   PSG_TRY(ensure_slots(s, r.n));
@@ -1474,7 +1518,7 @@ template <int DT>
 static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
   auto replay = [&](const InflightReq& g) {
     InflightReq r2;
-    int rc = launch_fused<DT>(s, g.op, g.q, g.n, g.vals, g.out, g.stream, &r2);
+    int rc = launch_fused<DT>(s, g.op, g.q, g.n, g.vals, g.out, g.stream, &r2, g.want_land != 0);
     if (rc == PSG_OK) {
       s->inflight.push_back(r2);
       int rc2 = PSG_OK;
@@ -1551,12 +1595,12 @@ static bool sorted_fused() {
 }
 
 static int launch_fused_any(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals, void* out,
-                            hipStream_t st, InflightReq* rec) {
+                            hipStream_t st, InflightReq* rec, bool want_land) {
   switch (s->dtype) {
-    case PSG_F32: return launch_fused<PSG_F32>(s, op, q, n, vals, out, st, rec);
-    case PSG_F64: return launch_fused<PSG_F64>(s, op, q, n, vals, out, st, rec);
-    case PSG_F16: return launch_fused<PSG_F16>(s, op, q, n, vals, out, st, rec);
-    default: return launch_fused<PSG_BF16>(s, op, q, n, vals, out, st, rec);
+    case PSG_F32: return launch_fused<PSG_F32>(s, op, q, n, vals, out, st, rec, want_land);
+    case PSG_F64: return launch_fused<PSG_F64>(s, op, q, n, vals, out, st, rec, want_land);
+    case PSG_F16: return launch_fused<PSG_F16>(s, op, q, n, vals, out, st, rec, want_land);
+    default: return launch_fused<PSG_BF16>(s, op, q, n, vals, out, st, rec, want_land);
   }
 }
 
@@ -1661,7 +1705,7 @@ static int handle_sync(psg_store* s, int flags, const uint64_t* keys, uint64_t f
   PSG_REQUIRE(keys, PSG_ERR_INVALID, "SORTED store needs explicit keys");
   if (!sorted_fused() || s->size == 0) return sorted_twopass(s, flags, keys, vals, out, n, st);
   InflightReq rec;
-  PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec));
+  PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec, true));
   s->inflight.push_back(rec);
   int own_rc = PSG_OK;
   PSG_TRY(reap(s, rec.ticket, rec.ticket, &own_rc));
@@ -1705,12 +1749,12 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
   if ((e = hipHostGetDevicePointer((void**)&s->flags, s->flags_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(flags)", __FILE__, __LINE__));
   memset(s->flags_host, 0, (F_NFLAGS + 1) * sizeof(int));
-  if ((e = hipHostMalloc((void**)&s->ring_host, kRing * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+  if ((e = hipHostMalloc((void**)&s->ring_host, 2 * kRing * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
       hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc(completion ring)", __FILE__, __LINE__));
   if ((e = hipHostGetDevicePointer((void**)&s->ring_dev, s->ring_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(completion ring)", __FILE__, __LINE__));
-  memset(s->ring_host, 0, kRing * sizeof(uint32_t));
+  memset(s->ring_host, 0, 2 * kRing * sizeof(uint32_t));  // completion words, then landed words
   if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
       (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(reject words)", __FILE__, __LINE__));
@@ -1823,7 +1867,7 @@ int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys, uint64
     PSG_TRY(reap(s, s->inflight.front().ticket, 0, &unused));
   }
   InflightReq rec;
-  PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec));
+  PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec, false));
   s->inflight.push_back(rec);
   *ticket = rec.ticket;
   return PSG_OK;
@@ -1833,6 +1877,11 @@ int psg_store_wait(psg_store* s, uint64_t ticket) {
   PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_wait: null store");
   int unused = PSG_OK;
   PSG_TRY(reap(s, ticket ? ticket : ~0ull, 0, &unused));
+  if (s->unlanded) {  // reaped Pulls' replies in memory
+    hipStream_t st = s->unlanded;
+    s->unlanded = nullptr;
+    PSG_HIP(hipStreamSynchronize(st));
+  }
   if (s->async_rc != PSG_OK) {
     const int rc = s->async_rc;
     s->async_rc = PSG_OK;

@@ -440,9 +440,8 @@ struct KVServerDefaultHandle {
       device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
                     "psg_store_handle");
       // psg_store_handle returns once the request's keys and vals are no longer
-      // read (psg.h), so a Push can be answered now; a Pull's reply must land
-      // first.  Later requests on this thread's stream are ordered behind it.
-      if (req_meta.pull) device::Check(psg_stream_sync(s), "psg_stream_sync");
+      // read and a Pull's reply is in memory (psg.h), so it can be answered
+      // now.  Later requests on this thread's stream are ordered behind it.
       if (state->key_cache) Remember(dkeys, on_dev, on_dev ? 0 : detail::KeyListHash(req_data.keys.data(), n), s);
     } else if (req_meta.push) {
       CHECK_EQ(n, req_data.vals.size());
