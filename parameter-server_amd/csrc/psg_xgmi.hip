@@ -30,7 +30,9 @@
 #include <atomic>
 #include <cerrno>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "psg_internal.h"
 
@@ -262,15 +264,53 @@ int psg_ipc_export(const void* dptr, void* handle_out) {
   return PSG_OK;
 }
 
+// Exported handles, by allocation: hipIpcGetMemHandle costs ~3 us a call on
+// MI355X (profiles/r3_probe_ipc_cost.txt), and the process-mode Van exports
+// every HBM frame of every request (keys, values, the direct-reply slice).  An
+// entry is keyed by the allocation's base AND its runtime buffer id (unique
+// per allocation, 0.07 us to read), so an address freed and allocated again
+// never reuses a stale handle.
+namespace {
+struct ExportEntry {
+  uint64_t buffer_id;
+  size_t size;
+  hipIpcMemHandle_t handle;
+};
+std::mutex g_export_mu;
+std::unordered_map<uintptr_t, ExportEntry> g_exports;
+constexpr size_t kMaxExports = 4096;
+}  // namespace
+
 int psg_ipc_export_range(const void* dptr, void* handle_out, uint64_t* offset_out) {
   PSG_REQUIRE(dptr && handle_out && offset_out, PSG_ERR_INVALID, "psg_ipc_export_range: null argument");
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   PSG_HIP(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)const_cast<void*>(dptr)));
+  static const bool cache_on = [] {  // PSG_IPC_EXPORT_CACHE=0: export every time (A/B)
+    const char* e = getenv("PSG_IPC_EXPORT_CACHE");
+    return !(e && atoi(e) == 0);
+  }();
+  unsigned long long id = 0;
+  const bool have_id = cache_on &&
+      hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, base) == hipSuccess && id != 0;
+  if (!have_id) (void)hipGetLastError();
+  *offset_out = (uint64_t)((const char*)dptr - (const char*)base);
+  if (have_id) {
+    std::lock_guard<std::mutex> lk(g_export_mu);
+    auto it = g_exports.find((uintptr_t)base);
+    if (it != g_exports.end() && it->second.buffer_id == id && it->second.size == size) {
+      memcpy(handle_out, &it->second.handle, sizeof(hipIpcMemHandle_t));
+      return PSG_OK;
+    }
+  }
   hipIpcMemHandle_t h;
   PSG_HIP(hipIpcGetMemHandle(&h, (void*)base));
   memcpy(handle_out, &h, sizeof(h));
-  *offset_out = (uint64_t)((const char*)dptr - (const char*)base);
+  if (have_id) {
+    std::lock_guard<std::mutex> lk(g_export_mu);
+    if (g_exports.size() >= kMaxExports) g_exports.clear();
+    g_exports[(uintptr_t)base] = ExportEntry{id, size, h};
+  }
   return PSG_OK;
 }
 
