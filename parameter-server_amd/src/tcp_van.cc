@@ -89,6 +89,38 @@ bool ReadAll(int fd, void* buf, size_t n) {
   return true;
 }
 
+// A connection's reader takes what the socket holds in one recv and serves the
+// message's small pieces (header, meta, frame descriptors) from it: one system
+// call per message instead of three per frame.  Payloads larger than the
+// buffer bypass it.
+struct SockReader {
+  int fd;
+  std::vector<char> buf = std::vector<char>(64 << 10);
+  size_t pos = 0, end = 0;
+  explicit SockReader(int f) : fd(f) {}
+  bool empty() const { return pos == end; }
+  bool read(void* out, size_t n) {
+    char* p = static_cast<char*>(out);
+    const size_t have = std::min(n, end - pos);
+    std::memcpy(p, buf.data() + pos, have);
+    pos += have;
+    p += have;
+    n -= have;
+    if (!n) return true;
+    if (n >= buf.size()) return ReadAll(fd, p, n);
+    pos = end = 0;
+    while (end < n) {
+      ssize_t r = ::recv(fd, buf.data() + end, buf.size() - end, 0);
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) return false;
+      end += (size_t)r;
+    }
+    std::memcpy(p, buf.data(), n);
+    pos = n;
+    return true;
+  }
+};
+
 // Before a connection's reader blocks in recv for the next message, poll the
 // socket for up to PS_SPIN_US (default 50 us, the spin of the request queues,
 // internal/customer.h): a request round trip crosses the socket twice, and a
@@ -858,18 +890,19 @@ SVector<char> TcpVan::MapShmFrame(int sender, const ShmFrame& f, uint64_t bytes)
 }
 
 void TcpVan::ReadLoop(int fd) {
+  SockReader rd(fd);
   int peer = Node::kEmpty;
   bool said_goodbye = false;
   while (true) {
     WireHeader wh;
-    SpinUntilReadable(fd);
-    if (!ReadAll(fd, &wh, sizeof(wh))) break;
+    if (rd.empty()) SpinUntilReadable(fd);
+    if (!rd.read(&wh, sizeof(wh))) break;
     if (wh.magic != kMagic) {
       LOG(ERROR) << "bad frame header from node " << peer << "; closing the connection";
       break;
     }
     std::string mb(wh.meta_bytes, '\0');
-    if (!ReadAll(fd, &mb[0], mb.size())) break;
+    if (!rd.read(&mb[0], mb.size())) break;
     Message msg;
     try {
       Reader r{mb.data(), mb.data() + mb.size()};
@@ -885,16 +918,16 @@ void TcpVan::ReadLoop(int fd) {
       std::vector<Pending> descs(wh.nframes);
       bool ok = true;
       for (auto& d : descs) {
-        ok = ok && ReadAll(fd, &d.kind, 1) && ReadAll(fd, &d.bytes, 8);
-        if (ok && d.kind == kIpcFrame) ok = ReadAll(fd, &d.ipc, sizeof(d.ipc));
-        if (ok && d.kind == kPeerFrame) ok = ReadAll(fd, &d.peer, sizeof(d.peer));
-        if (ok && d.kind == kShmFrame) ok = ReadAll(fd, &d.shm, sizeof(d.shm));
+        ok = ok && rd.read(&d.kind, 1) && rd.read(&d.bytes, 8);
+        if (ok && d.kind == kIpcFrame) ok = rd.read(&d.ipc, sizeof(d.ipc));
+        if (ok && d.kind == kPeerFrame) ok = rd.read(&d.peer, sizeof(d.peer));
+        if (ok && d.kind == kShmFrame) ok = rd.read(&d.shm, sizeof(d.shm));
       }
       if (!ok) break;
       for (auto& d : descs) {
         if (d.kind == kHostFrame) {
           SVector<char> h = SVector<char>::Uninitialized(d.bytes);
-          if (d.bytes && !ReadAll(fd, h.data(), d.bytes)) {
+          if (d.bytes && !rd.read(h.data(), d.bytes)) {
             ok = false;
             break;
           }
