@@ -495,13 +495,57 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
   uint64_t after = 0;
   bool arrived = false;
   const uint64_t ntiles = skip ? 0 : (n + tileN - 1) / tileN;
+  // A tile's inputs that do not depend on its window — its window entry, its
+  // request keys, the key before a wave's first (CHECK) and (Push) its values
+  // — are loaded one tile ahead (pf), while the current tile's store values
+  // are in flight: a tile then waits on two dependent HBM round trips (its
+  // window, then its store values) instead of three (entry, window, values).
+  uint64_t nkey[kPerLane] = {}, nprev = 0, nqfirst = 0, nqlast = 0;
+  T nv[kPerLane] = {};
+  Win ne = {};
+  auto load_tile = [&](uint64_t tl) {
+    const uint64_t a0 = tl * tileN;
+    const uint64_t a1 = (a0 + tileN < n) ? a0 + tileN : n;
+    const uint64_t j0 = a0 + (uint64_t)threadIdx.x * kPerLane;
+    ne = win[tl];
+    nqfirst = q[a0];
+    nqlast = q[a1 - 1];
+    if (j0 + kPerLane <= a1 && (vec & 2)) {
+      const u64x2 a = *reinterpret_cast<const u64x2*>(q + j0);
+      const u64x2 b = *reinterpret_cast<const u64x2*>(q + j0 + 2);
+      nkey[0] = a[0];
+      nkey[1] = a[1];
+      nkey[2] = b[0];
+      nkey[3] = b[1];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) nkey[k] = j0 + k < a1 ? q[j0 + k] : 0;
+    }
+    if constexpr (CHECK) nprev = ((threadIdx.x & 63) == 0 && j0 > 0 && j0 < a1) ? q[j0 - 1] : 0;
+    if constexpr ((OP & PSG_PUSH) != 0) {
+      bool vdone = false;
+      if constexpr (sizeof(T) == 4) {
+        if (j0 + kPerLane <= a1 && (vec & 1)) {
+          const f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(vals + j0));
+#pragma unroll
+          for (int k = 0; k < kPerLane; ++k) nv[k] = x[k];
+          vdone = true;
+        }
+      }
+      if (!vdone) {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) nv[k] = (j0 + k < a1) ? vals[j0 + k] : (T)0.0f;
+      }
+    }
+  };
+  if (blockIdx.x < ntiles) load_tile(blockIdx.x);
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * tileN;
     const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
     // the window cached for this tile, staged speculatively: it is right when
     // it was computed against this K for this tile's first and last key
-    // (checked below, once those keys have arrived with the rest)
-    const Win e = win[tile];
+    // (checked below)
+    const Win e = ne;
     const bool cur = e.gen == gen;
     uint64_t lo = cur ? e.lo : 0, hi = cur ? e.hi : 0;
     if (hi > S) hi = S;
@@ -510,25 +554,11 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
     bool staged = W <= (uint64_t)winN;
     const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
     const bool whole = i0 + kPerLane <= t1;
-    // Issue every global load that does not depend on the window before the
-    // barrier — the window's store keys, this lane's request keys, the key
-    // before them and (Push) its values — so a tile costs two dependent HBM
-    // round trips (these, then the store values) instead of one per staging
-    // step plus two.
     if (cur && staged) stage_window<NT>(sK, K, lo, W);
-    const uint64_t qfirst = q[t0], qlast = q[t1 - 1];
+    const uint64_t qfirst = nqfirst, qlast = nqlast;
     uint64_t key[kPerLane];
-    if (whole && (vec & 2)) {
-      const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0);
-      const u64x2 b = *reinterpret_cast<const u64x2*>(q + i0 + 2);
-      key[0] = a[0];
-      key[1] = a[1];
-      key[2] = b[0];
-      key[3] = b[1];
-    } else {
 #pragma unroll
-      for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : 0;
-    }
+    for (int k = 0; k < kPerLane; ++k) key[k] = nkey[k];
     if constexpr (CHECK) {
       // strict ascent against the key before this lane's four (the previous
       // lane's last, by a shuffle; lane 0 of a wave loads it) and the range
@@ -538,7 +568,7 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
       bool have_prev = true;
       if ((threadIdx.x & 63) == 0) {
         have_prev = i0 > 0 && i0 < t1;
-        prev = have_prev ? q[i0 - 1] : 0;
+        prev = nprev;
       }
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) {
@@ -551,21 +581,8 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
       }
     }
     T v[kPerLane];
-    if constexpr ((OP & PSG_PUSH) != 0) {
-      if constexpr (sizeof(T) == 4) {
-        if (whole && (vec & 1)) {
-          const f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(vals + i0));
 #pragma unroll
-          for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
-        } else {
-#pragma unroll
-          for (int k = 0; k < kPerLane; ++k) v[k] = (i0 + k < t1) ? vals[i0 + k] : (T)0.0f;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kPerLane; ++k) v[k] = (i0 + k < t1) ? vals[i0 + k] : (T)0.0f;
-      }
-    }
+    for (int k = 0; k < kPerLane; ++k) v[k] = nv[k];
     // The window reaches LDS by DMA (global_load_lds), which only vmcnt
     // tracks; the barrier's workgroup fence does not wait on it in
     // non-tgsplit mode.  Wait explicitly so no wave reads another wave's part
@@ -633,6 +650,9 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
                            &s_cond, arrival);
       arrived = true;
     }
+    // the next tile's inputs, issued ahead of this tile's store values below
+    // (the compiler's vmcnt waits let those return first)
+    if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x);
     // apply.  A lane whose 4 keys are 4 consecutive, 16-B aligned store
     // slots (the common case: a request that covers a stretch of the store)
     // moves its store values as one vector; request values and replies are one

@@ -8,8 +8,8 @@
 #   keyed    keyed bench lines (configs[3]:    proffk / profkc  rocprof kernel stats of
 #            uncached and key-cached)                  keyed / keyed-cached
 #   f16      1 G f16 bench line (configs[4])   e2e    C++ API end to end, 10 M keys
-#   t:EXPR   pytest -m gpu -k EXPR             pmck / pmckc  PMC traffic of the keyed /
-#                                                      key-cached Push (two passes each)
+#   t:EXPR   pytest -m gpu -k EXPR             pmck / pmckc / pmckp  PMC traffic of the keyed /
+#                                                      key-cached Push, keyed Pull (two passes each)
 #   trace    kernel trace of the keyed bench: durations and the idle gaps between
 #            launches (tools/trace_gaps.py)
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
@@ -38,8 +38,9 @@ for st in "$@"; do
     profkc) rm -rf gpurun_out/prof_keyed_cached
           step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_keyed_cached -o run --output-format csv -- python3 bench.py --workload keyed-cached --no-cpu-baseline --steps 20 > gpurun_out/prof_keyed_cached.json 2>&1; echo "profkc rc=$?"
           f=$(find gpurun_out/prof_keyed_cached -name "*kernel_stats.csv" | head -1); cut -c1-160 "$f" | head -8 ;;
-    pmck|pmckc)
+    pmck|pmckc|pmckp)
           if [ "$st" = pmck ]; then wl=keyed; ks="k_validate_windows|k_resolve_apply<0, 1,"; per=28; out=pmc_keyed_push_traffic.json
+          elif [ "$st" = pmckp ]; then wl=keyed; ks="k_resolve_apply<0, 2,"; per=24; out=pmc_keyed_pull_traffic.json
           else wl=keyed-cached; ks="k_slots_vec<0, 1,"; per=16; out=pmc_keyed_cached_push_traffic.json; fi
           rm -rf gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st
           step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
