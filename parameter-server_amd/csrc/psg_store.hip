@@ -650,43 +650,41 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
                            &s_cond, arrival);
       arrived = true;
     }
-    // the next tile's inputs, issued ahead of this tile's store values below
-    // (the compiler's vmcnt waits let those return first)
-    if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x);
     // apply.  A lane whose 4 keys are 4 consecutive, 16-B aligned store
     // slots (the common case: a request that covers a stretch of the store)
     // moves its store values as one vector; request values and replies are one
     // vector when T is 4 B, the tile is whole and the caller's arrays are 16-B
     // aligned (vec & 1, checked on the host)
-    T o[kPerLane];
-    bool done_v = false;
-    if constexpr (sizeof(T) == 4) {
-      if (hit[0] && hit[1] && hit[2] && hit[3] && slot[3] == slot[0] + 3 && (slot[0] & 3) == 0) {
-        const f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + slot[0]));
-        T y[kPerLane];
+    T o[kPerLane], x[kPerLane];
+    bool vecv = false;
+    if constexpr (sizeof(T) == 4)
+      vecv = hit[0] && hit[1] && hit[2] && hit[3] && slot[3] == slot[0] + 3 && (slot[0] & 3) == 0;
+    if (vecv) {
+      if constexpr (sizeof(T) == 4) {
+        const f32x4 xv = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + slot[0]));
 #pragma unroll
-        for (int k = 0; k < kPerLane; ++k) {
-          y[k] = x[k];
-          if constexpr ((OP & PSG_PUSH) != 0) y[k] = E::add1(y[k], v[k]);
-          o[k] = y[k];
-        }
-        if constexpr ((OP & PSG_PUSH) != 0)
-          *reinterpret_cast<u32x4*>(V + slot[0]) = __builtin_bit_cast(u32x4, f32x4{y[0], y[1], y[2], y[3]});
-        done_v = true;
+        for (int k = 0; k < kPerLane; ++k) x[k] = xv[k];
       }
-    }
-    if (!done_v) {
+    } else {
 #pragma unroll
-      for (int k = 0; k < kPerLane; ++k) {
-        T x = (T)0.0f;
-        if (hit[k]) {
-          x = V[slot[k]];
-          if constexpr ((OP & PSG_PUSH) != 0) {
-            x = E::add1(x, v[k]);
-            V[slot[k]] = x;
-          }
-        }
-        o[k] = x;
+      for (int k = 0; k < kPerLane; ++k) x[k] = hit[k] ? V[slot[k]] : (T)0.0f;
+    }
+    // the next tile's inputs, issued behind this tile's store values (whose
+    // waits then leave them in flight)
+    if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x);
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      o[k] = x[k];
+      if constexpr ((OP & PSG_PUSH) != 0) o[k] = E::add1(x[k], v[k]);
+    }
+    if constexpr ((OP & PSG_PUSH) != 0) {
+      if (vecv) {
+        if constexpr (sizeof(T) == 4)
+          *reinterpret_cast<u32x4*>(V + slot[0]) = __builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]});
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k)
+          if (hit[k]) V[slot[k]] = o[k];
       }
     }
     if constexpr ((OP & PSG_PULL) != 0) {
