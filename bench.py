@@ -827,12 +827,24 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                                    "from the one resolve of the key list)", vb)
         res["pull_roofline_frac"] = round(12 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     elif world == 1 and getattr(backend, "keyed", False):
-        res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args,
-                                   "SORTED-store Push: k_validate_windows + k_resolve_apply "
-                                   "(whole-request validation before any write; tile windows "
-                                   "cached per key array; requests in flight, each reporting "
-                                   "completion and flags in one kernel-written word; one "
-                                   "server, so no slicer pass)", vb)
+        # which kernels served the run's keyed requests (psg_store_counters):
+        # the identity pair once the key list's windows are trusted
+        paths = backend.store.counters()
+        res["keyed_paths"] = paths
+        if paths["ident"] > 0 and paths["notident"] == 0:
+            kname = ("SORTED-store Push: k_ident_check + k_ident_apply (identity request: the key "
+                     "list covers a stretch of the store, so key i of a tile sits at its cached "
+                     "window's slot lo + i; the check — request key = store key, 16 B/key — is the "
+                     "whole validation, then values only, 12 B/key; requests in flight, each "
+                     "reporting completion and flags in one kernel-written word; one server, so "
+                     "no slicer pass)")
+        else:
+            kname = ("SORTED-store Push: k_validate_windows + k_resolve_apply "
+                     "(whole-request validation before any write; tile windows "
+                     "cached per key array; requests in flight, each reporting "
+                     "completion and flags in one kernel-written word; one "
+                     "server, so no slicer pass)")
+        res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args, kname, vb)
         res["pull_roofline_frac"] = round(24 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,

@@ -166,6 +166,20 @@ int psg_store_destroy(psg_store* s);
 int psg_store_get_info(psg_store* s, psg_store_info* info);
 /* Zero every value (DENSE) / drop every key (SORTED). */
 int psg_store_clear(psg_store* s, psg_stream stream);
+/* How a SORTED store served its keyed requests so far (diagnostics and tests;
+ * no reference counterpart): out[PSG_CTR_FUSED] requests on the validated
+ * resolve-and-apply kernels, [PSG_CTR_IDENT] sent as identity requests (a key
+ * list covering stretches of the store, at slots known from its cached
+ * windows: no validation pass, no search), [PSG_CTR_NOTIDENT] of those that
+ * were not and ran again on the general path, [PSG_CTR_ORDERED] on the
+ * order-preserving path (keys out of order or repeated).  Waits for the
+ * requests in flight.  Writes min(n, PSG_NCOUNTERS) counters, zero past them. */
+#define PSG_CTR_FUSED 0
+#define PSG_CTR_IDENT 1
+#define PSG_CTR_NOTIDENT 2
+#define PSG_CTR_ORDERED 3
+#define PSG_NCOUNTERS 4
+int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):
  *   for i < n:  if (flags & PSG_PUSH) store[key_i] += vals[i];

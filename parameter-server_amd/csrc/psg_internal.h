@@ -150,6 +150,7 @@ struct InflightReq {
   hipStream_t stream;
   int want_land;  // a Pull answered when reaped (psg_store_handle): its reply must be in memory then
   int land;       // ... and the stream writes tag to ring_host[kRing + ring] after the kernel to say so
+  int ident;      // sent as an identity request (k_ident_check / k_ident_apply)
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
 }  // namespace psg
@@ -212,8 +213,10 @@ struct psg_store {
     uint64_t last_use;
     int trusted;         // skip the search pre-pass; the kernel still verifies
     int strikes;         // kernel-detected stale windows for this (q, n)
+    uint32_t ident_fail; // K's generation at which an identity request on this list was not one
   } wc[4];
   uint64_t wc_clock;
+  uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters
 };
 
 struct psg_adam {

@@ -40,7 +40,7 @@ EXPORTS = [
     "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
     "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",
-    "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear",
+    "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear", "psg_store_counters",
     "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
     "psg_key_list_hash",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
@@ -110,6 +110,7 @@ def lib() -> C.CDLL:
             "psg_store_destroy": ([vp], i32),
             "psg_store_get_info": ([vp, C.POINTER(StoreInfo)], i32),
             "psg_store_clear": ([vp, vp], i32),
+            "psg_store_counters": ([vp, C.POINTER(C.c_uint64), i32], i32),
             "psg_store_handle": ([vp, i32, vp, u64, vp, vp, u64, vp], i32),
             "psg_store_handle_async": ([vp, i32, vp, u64, vp, vp, u64, vp, C.POINTER(u64)], i32),
             "psg_store_wait": ([vp, u64], i32),
@@ -345,6 +346,12 @@ class Store:
         i = StoreInfo()
         _call("psg_store_get_info", self.h, C.byref(i))
         return i
+
+    def counters(self) -> dict:
+        """How the store served its keyed requests (psg_store_counters)."""
+        c = (C.c_uint64 * 4)()
+        _call("psg_store_counters", self.h, c, 4)
+        return {"fused": c[0], "ident": c[1], "notident": c[2], "ordered": c[3]}
 
     def handle(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> None:
         _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,

