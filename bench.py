@@ -833,11 +833,11 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         res["keyed_paths"] = paths
         if paths["ident"] > 0 and paths["notident"] == 0:
             kname = ("SORTED-store Push: k_ident_check + k_ident_apply (identity request: the key "
-                     "list covers a stretch of the store, so key i of a tile sits at its cached "
-                     "window's slot lo + i; the check — request key = store key, 16 B/key — is the "
-                     "whole validation, then values only, 12 B/key; requests in flight, each "
-                     "reporting completion and flags in one kernel-written word; one server, so "
-                     "no slicer pass)")
+                     "list is the stretch K[D, D + n) of the store's keys, D from its first tile's "
+                     "cached window, so key i sits at slot D + i; the check — request key = store "
+                     "key, 16 B/key — is the whole validation, then values only, 12 B/key; "
+                     "requests in flight, each reporting completion and flags in one "
+                     "kernel-written word; one server, so no slicer pass)")
         else:
             kname = ("SORTED-store Push: k_validate_windows + k_resolve_apply "
                      "(whole-request validation before any write; tile windows "
