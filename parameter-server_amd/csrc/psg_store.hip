@@ -738,6 +738,8 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
 // W_NOTIDENT, raising kPending like any follow-up, and the host serves it again
 // on the general path.
 
+constexpr int kIdU = 2;  // groups of 4 keys in flight per lane
+
 // The stretch's first slot, uniform: tile 0's cached window is current and is
 // for this first key, and n slots fit from it.
 __device__ __forceinline__ bool stretch_base(const uint64_t* __restrict__ q, uint64_t n, uint64_t S,
@@ -763,15 +765,26 @@ __global__ __launch_bounds__(256) void k_ident_check(const uint64_t* __restrict_
     const uint64_t* Kd = K + D;
     uint64_t done = 0;
     if ((vec & 2) && (D & 1) == 0) {
-      // 4 keys per lane: two 16-B loads of each array
+      // groups of 4 keys (two 16-B loads of each array), kIdU groups per lane
+      // in flight, blocks striding over kBlock * kIdU-group tiles
       const uint64_t ng = n / 4;
       done = ng * 4;
-      for (uint64_t j = gid; j < ng; j += stride) {
-        const u64x2 a = *reinterpret_cast<const u64x2*>(q + 4 * j);
-        const u64x2 b = *reinterpret_cast<const u64x2*>(q + 4 * j + 2);
-        const u64x2 c = *reinterpret_cast<const u64x2*>(Kd + 4 * j);
-        const u64x2 d = *reinterpret_cast<const u64x2*>(Kd + 4 * j + 2);
-        if (a[0] != c[0] || a[1] != c[1] || b[0] != d[0] || b[1] != d[1]) bad = 1;
+      for (uint64_t b = (uint64_t)blockIdx.x * kBlock * kIdU + threadIdx.x; b < ng; b += stride * kIdU) {
+        u64x2 a[kIdU][2], c[kIdU][2];
+#pragma unroll
+        for (int u = 0; u < kIdU; ++u) {
+          const uint64_t j = b + (uint64_t)u * kBlock < ng ? b + (uint64_t)u * kBlock : b;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            a[u][h] = *reinterpret_cast<const u64x2*>(q + 4 * j + 2 * h);
+            c[u][h] = *reinterpret_cast<const u64x2*>(Kd + 4 * j + 2 * h);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kIdU; ++u)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (a[u][h][0] != c[u][h][0] || a[u][h][1] != c[u][h][1]) bad = 1;
       }
     }
     for (uint64_t i = done + gid; i < n; i += stride)
@@ -822,22 +835,48 @@ __global__ __launch_bounds__(256) void k_ident_apply(const uint64_t* __restrict_
       if constexpr (sizeof(T) == 4) {
         const uint64_t ng = n / 4;
         done = ng * 4;
-        for (uint64_t j = gid; j < ng; j += stride) {
-          f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(Vd + 4 * j));
-          if constexpr (PUSH) {
-            const f32x4 v = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(vals + 4 * j));
+        for (uint64_t b = (uint64_t)blockIdx.x * kBlock * kIdU + threadIdx.x; b < ng; b += stride * kIdU) {
+          // kIdU groups of 4 per lane in flight (a lane past the end repeats
+          // its first group, unwritten)
+          f32x4 x[kIdU], v[kIdU];
+          u64x2 a[kIdU][2], c[kIdU][2];
+          uint64_t j[kIdU];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) x[k] = E::add1(x[k], v[k]);
-            *reinterpret_cast<u32x4*>(Vd + 4 * j) = __builtin_bit_cast(u32x4, x);
-          } else {
-            const u64x2 a = *reinterpret_cast<const u64x2*>(q + 4 * j);
-            const u64x2 b = *reinterpret_cast<const u64x2*>(q + 4 * j + 2);
-            const u64x2 c = *reinterpret_cast<const u64x2*>(Kd + 4 * j);
-            const u64x2 d = *reinterpret_cast<const u64x2*>(Kd + 4 * j + 2);
-            if (a[0] != c[0] || a[1] != c[1] || b[0] != d[0] || b[1] != d[1]) bad = 1;
+          for (int u = 0; u < kIdU; ++u) {
+            j[u] = b + (uint64_t)u * kBlock < ng ? b + (uint64_t)u * kBlock : b;
+            x[u] = __builtin_bit_cast(f32x4, (vec & 8) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Vd + 4 * j[u]))
+                                                       : *reinterpret_cast<const u32x4*>(Vd + 4 * j[u]));
+            if constexpr (PUSH) {
+              v[u] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals) + j[u]));
+            } else {
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                a[u][h] = *reinterpret_cast<const u64x2*>(q + 4 * j[u] + 2 * h);
+                c[u][h] = *reinterpret_cast<const u64x2*>(Kd + 4 * j[u] + 2 * h);
+              }
+            }
           }
-          if constexpr (PULL)
-            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x), reinterpret_cast<u32x4*>(outv + 4 * j));
+#pragma unroll
+          for (int u = 0; u < kIdU; ++u) {
+            const bool in = b + (uint64_t)u * kBlock < ng;
+            if constexpr (PUSH) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) x[u][k] = E::add1(x[u][k], v[u][k]);
+              if (in) {
+                if (vec & 4)
+                  __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x[u]), reinterpret_cast<u32x4*>(Vd + 4 * j[u]));
+                else
+                  *reinterpret_cast<u32x4*>(Vd + 4 * j[u]) = __builtin_bit_cast(u32x4, x[u]);
+              }
+            } else {
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                if (a[u][h][0] != c[u][h][0] || a[u][h][1] != c[u][h][1]) bad = 1;
+            }
+            if constexpr (PULL)
+              if (in)
+                __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x[u]), reinterpret_cast<u32x4*>(outv) + j[u]);
+          }
         }
       }
     }
@@ -1509,9 +1548,14 @@ template <int DT, int OP>
 static void launch_ident(psg_store* s, const uint64_t* q, uint64_t n, const void* vals, void* out, const Win* win,
                          const InflightReq& rec, hipStream_t st) {
   using T = typename Elem<DT>::T;
-  const unsigned g = grid_n(n, (uint64_t)kBlock * 4);
+  const unsigned g = grid_n(n, (uint64_t)kBlock * 4 * kIdU);
+  // PSG_ID_NT (A/B): bit 0 the store values written non-temporally, bit 1 read so
+  static const int id_nt = [] {
+    const char* e = getenv("PSG_ID_NT");
+    return e ? atoi(e) : 0;
+  }();
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
-                  (aligned16(q) ? 2 : 0);
+                  (aligned16(q) ? 2 : 0) | ((id_nt & 1) ? 4 : 0) | ((id_nt & 2) ? 8 : 0);
   if (OP & PSG_PUSH)
     k_ident_check<<<g, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->reject_dev, s->seq, vec);
   Arrival arr;
