@@ -62,6 +62,8 @@ WORKLOADS = {
 KEYED_PUSH_BYTES = 28
 # ... and with a cached slot list: slot 4 + value 4 + store value read/write 8
 CACHED_PUSH_BYTES = 16
+# ... and when that list's slots are a stretch of the store: value 4 + store value read/write 8
+STRETCH_PUSH_BYTES = 12
 # pushes outside warmup + steps that a run may make (calibration, verification)
 EXTRA_PUSH_BOUND = 64
 
@@ -119,6 +121,10 @@ class GpuBackend:
             # run on the cached slots
             self.slots = p.DeviceBuffer(L * 4)
             self.store.resolve(self.keys, L, self.slots, insert=True, stream=self.stream)
+            # a list that covers its range of the store resolves to a stretch of
+            # slots, served without the slot stream (psg_store_handle_stretch)
+            self.stretch = None if os.environ.get("PSG_BENCH_NO_STRETCH") == "1" else \
+                self.store.slots_stretch(self.slots, L, stream=self.stream)
         if self.world > 1 and self.cached:
             self._setup_keyed_cached()
         elif self.world > 1:
@@ -277,7 +283,9 @@ class GpuBackend:
             # writes this rank's own shard out once its own Push is done
             self.xgmi.push(self.store, self.L, self.stream)
             return
-        if self.cached:
+        if self.cached and getattr(self, "stretch", None) is not None:
+            self.store.handle_stretch(self.p.PUSH, self.stretch, self.vals, None, self.L, stream=self.stream)
+        elif self.cached:
             self.store.handle_slots(self.p.PUSH, self.slots, self.vals, None, self.L, stream=self.stream)
         elif self.keyed:
             # one server: the slice is the whole request (KVWorker's DefaultSlicer
@@ -321,7 +329,9 @@ class GpuBackend:
             self.stream.sync()
             self.node_barrier.wait()
             return
-        if self.cached:
+        if self.cached and getattr(self, "stretch", None) is not None:
+            self.store.handle_stretch(self.p.PULL, self.stretch, None, self.out, self.L, stream=self.stream)
+        elif self.cached:
             self.store.handle_slots(self.p.PULL, self.slots, None, self.out, self.L, stream=self.stream)
         elif self.keyed:
             if self.comm is None:
@@ -821,7 +831,16 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
             res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
         if getattr(backend, "share_gpu", False):
             res["config"]["shared_gpu_test_mode"] = True
-    if world == 1 and getattr(backend, "cached", False):
+    if world == 1 and getattr(backend, "cached", False) and getattr(backend, "stretch", None) is not None:
+        # the cached list resolved to a stretch of slots: no slot stream, so the
+        # request's bytes are those of the dense op on that stretch
+        res["roofline"] = roofline(STRETCH_PUSH_BYTES * L, push_ms, args,
+                                   "cached-list Push on a stretch of slots: k_dense_vec<PUSH> on "
+                                   "store[first, first + n) (psg_store_handle_stretch; the list's one "
+                                   "resolve found slots[i] == first + i)", vb)
+        res["pull_roofline_frac"] = round(8 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        res["config"]["cached_slots"] = "stretch from slot %d" % backend.stretch
+    elif world == 1 and getattr(backend, "cached", False):
         res["roofline"] = roofline(CACHED_PUSH_BYTES * L, push_ms, args,
                                    "cached-slot Push: k_slots_vec (store[slot] += val, slots "
                                    "from the one resolve of the key list)", vb)

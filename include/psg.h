@@ -250,6 +250,18 @@ int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert
 int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots,
                            const void* vals, void* out, uint64_t n,
                            psg_stream stream);
+/* A slot list that is a stretch of the store — slots[i] == slots[0] + i for
+ * every i, as when a cached key list covers its range of the store (an LR
+ * worker sending every feature, tests/src/LRServer.h:144) — needs no slot
+ * stream: *first = slots[0] then, else UINT64_MAX.  Synchronises `stream`.
+ * psg_store_handle_stretch is then psg_store_handle_slots on the slots
+ * [first, first + n): store[first + i] += vals[i] and / or out[i] =
+ * store[first + i], a plain stream (12 B / f32 key for a Push instead of 16,
+ * 8 for a Pull instead of 12).  Slots stay valid until the next insert. */
+int psg_store_slots_stretch(psg_store* s, const uint32_t* slots, uint64_t n, uint64_t* first,
+                            psg_stream stream);
+int psg_store_handle_stretch(psg_store* s, int flags, uint64_t first, const void* vals, void* out,
+                             uint64_t n, psg_stream stream);
 
 /* The hash a key list is cached under in LR key caching (the std::hash
  * specialisation of tests/src/LRServer.h:11-29, which LRWorker.h:214-219 also

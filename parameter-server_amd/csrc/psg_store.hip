@@ -895,6 +895,18 @@ __global__ __launch_bounds__(256) void k_ident_apply(const uint64_t* __restrict_
   request_done(after, arrival, uniform, rej + kPending, word, tag_bits, W_NOTIDENT);
 }
 
+// A slot list that is a stretch of the store: slots[i] == slots[0] + i for
+// every i (psg_store_slots_stretch).  Any other list raises F_MISSING (here:
+// "not a stretch").
+__global__ __launch_bounds__(256) void k_slots_stretch(const uint32_t* __restrict__ slots, uint64_t n,
+                                                       int* __restrict__ flags) {
+  const uint64_t s0 = slots[0];
+  int bad = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+    if ((uint64_t)slots[i] != s0 + i) bad = 1;
+  raise_flag(flags, F_MISSING, bad != 0);
+}
+
 // Block-wide exclusive scan helper over 256 lanes (wave = 64).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total) {
   __shared__ uint32_t wsum[4];
@@ -2186,6 +2198,42 @@ int psg_store_resolve(psg_store* s, const uint64_t* keys, uint64_t n, int insert
   PSG_TRY(sorted_resolve(s, keys, n, insert != 0, st));
   PSG_HIP(hipMemcpyAsync(slots, s->slots, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return PSG_OK;
+}
+
+int psg_store_slots_stretch(psg_store* s, const uint32_t* slots, uint64_t n, uint64_t* first,
+                            psg_stream stream) {
+  PSG_REQUIRE(s && first, PSG_ERR_INVALID, "psg_store_slots_stretch: null argument");
+  *first = UINT64_MAX;
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(slots, PSG_ERR_INVALID, "psg_store_slots_stretch: null slots");
+  PSG_TRY(drain(s));
+  hipStream_t st = (hipStream_t)stream;
+  reset_flags(s);
+  k_slots_stretch<<<grid_n(n, kBlock), kBlock, 0, st>>>(slots, n, s->flags);
+  PSG_HIP(hipGetLastError());
+  PSG_TRY(read_flags(s, st));
+  if (s->flags_host[F_MISSING]) return PSG_OK;
+  uint32_t s0 = 0;
+  PSG_HIP(hipMemcpy(&s0, slots, sizeof(s0), hipMemcpyDeviceToHost));
+  const uint64_t limit = s->kind == PSG_STORE_SORTED ? s->size : s->capacity;
+  if (s0 != kNoSlot && (uint64_t)s0 <= limit && n <= limit - s0) *first = s0;
+  return PSG_OK;
+}
+
+int psg_store_handle_stretch(psg_store* s, int flags, uint64_t first, const void* vals, void* out, uint64_t n,
+                             psg_stream stream) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_handle_stretch: null store");
+  PSG_REQUIRE(flags >= 1 && flags <= 3, PSG_ERR_INVALID, "bad flags %d", flags);
+  if (n == 0) return PSG_OK;
+  PSG_REQUIRE(!(flags & PSG_PUSH) || vals, PSG_ERR_INVALID, "push without vals");
+  PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
+  PSG_TRY(drain(s));
+  const uint64_t limit = s->kind == PSG_STORE_SORTED ? s->size : s->capacity;
+  PSG_REQUIRE(first <= limit && n <= limit - first, PSG_ERR_RANGE,
+              "psg_store_handle_stretch: slots [%llu, %llu) past the store's %llu", (unsigned long long)first,
+              (unsigned long long)(first + n), (unsigned long long)limit);
+  return dense_request(s->dtype, flags, static_cast<char*>(s->vals) + first * (uint64_t)s->esize, vals, out, n,
+                       (hipStream_t)stream);
 }
 
 int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots, const void* vals,

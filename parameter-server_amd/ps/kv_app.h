@@ -387,6 +387,10 @@ struct KVServerDefaultHandle {
     SVector<Key> keys;        // the list (HBM), kept for a re-resolve
     SVector<uint32_t> slots;  // its store slots (HBM)
     uint64_t store_size = 0;  // the store's size when resolved (an insert moves slots)
+    // the first slot when the slots are a stretch of the store (the list covers
+    // its range: LRServer.h:144's every-feature list), else UINT64_MAX: then a
+    // request needs no slot stream (psg_store_handle_stretch)
+    uint64_t stretch = UINT64_MAX;
   };
   struct State {
     psg_store* store = nullptr;
@@ -428,8 +432,12 @@ struct KVServerDefaultHandle {
       SVector<Value> dvals;
       if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
       if (req_meta.pull) dout = PullOutput(server, n, dev, &direct);
-      device::Check(psg_store_handle_slots(state->store, flags, c.slots.data(), dvals.data(), dout.data(), n, s),
-                    "psg_store_handle_slots");
+      if (c.stretch != UINT64_MAX)
+        device::Check(psg_store_handle_stretch(state->store, flags, c.stretch, dvals.data(), dout.data(), n, s),
+                      "psg_store_handle_stretch");
+      else
+        device::Check(psg_store_handle_slots(state->store, flags, c.slots.data(), dvals.data(), dout.data(), n, s),
+                      "psg_store_handle_slots");
       device::Check(psg_stream_sync(s), "psg_stream_sync");
     } else if (n && flags) {
       if (req_meta.push) CHECK_EQ(n, req_data.vals.size());
@@ -504,7 +512,7 @@ struct KVServerDefaultHandle {
     }
     c.slots = SVector<uint32_t>::OnDevice(n, dev);
     device::Check(psg_store_resolve(state->store, c.keys.data(), n, 0, c.slots.data(), s), "psg_store_resolve");
-    device::Check(psg_stream_sync(s), "psg_stream_sync");
+    device::Check(psg_store_slots_stretch(state->store, c.slots.data(), n, &c.stretch, s), "psg_store_slots_stretch");
     c.store_size = StoreSize();
     state->cache.emplace(h, std::move(c));
   }
@@ -513,7 +521,8 @@ struct KVServerDefaultHandle {
     if (size == c.store_size) return;
     device::Check(psg_store_resolve(state->store, c.keys.data(), c.keys.size(), 0, c.slots.data(), s),
                   "psg_store_resolve");
-    device::Check(psg_stream_sync(s), "psg_stream_sync");
+    device::Check(psg_store_slots_stretch(state->store, c.slots.data(), c.keys.size(), &c.stretch, s),
+                  "psg_store_slots_stretch");
     c.store_size = size;
   }
 };

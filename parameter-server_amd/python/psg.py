@@ -41,7 +41,8 @@ EXPORTS = [
     "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear", "psg_store_counters",
-    "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots", "psg_store_dump",
+    "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots",
+    "psg_store_slots_stretch", "psg_store_handle_stretch", "psg_store_dump",
     "psg_key_list_hash",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
@@ -117,6 +118,8 @@ def lib() -> C.CDLL:
             "psg_sort_pairs_u64": ([vp, vp, u64, i32, vp], i32),
             "psg_store_resolve": ([vp, vp, u64, i32, vp, vp], i32),
             "psg_store_handle_slots": ([vp, i32, vp, vp, vp, u64, vp], i32),
+            "psg_store_slots_stretch": ([vp, vp, u64, C.POINTER(u64), vp], i32),
+            "psg_store_handle_stretch": ([vp, i32, u64, vp, vp, u64, vp], i32),
             "psg_store_dump": ([vp, vp, vp], i32),
             "psg_key_list_hash": ([vp, u64, C.POINTER(u64), vp], i32),
             "psg_server_ranges": ([i32, vp, vp], i32),
@@ -374,6 +377,16 @@ class Store:
     def handle_slots(self, flags: int, slots, vals, out, n: int, stream=None) -> None:
         _call("psg_store_handle_slots", self.h, flags, _ptr(slots), _ptr(vals), _ptr(out), n,
               _s(stream))
+
+    def slots_stretch(self, slots, n: int, stream=None):
+        """The first slot when slots[i] == slots[0] + i for every i, else None
+        (psg_store_slots_stretch)."""
+        f = C.c_uint64(0)
+        _call("psg_store_slots_stretch", self.h, _ptr(slots), n, C.byref(f), _s(stream))
+        return None if f.value == (1 << 64) - 1 else f.value
+
+    def handle_stretch(self, flags: int, first: int, vals, out, n: int, stream=None) -> None:
+        _call("psg_store_handle_stretch", self.h, flags, first, _ptr(vals), _ptr(out), n, _s(stream))
 
     def clear(self, stream=None) -> None:
         _call("psg_store_clear", self.h, _s(stream))

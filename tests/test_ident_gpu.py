@@ -231,3 +231,46 @@ print(st.counters()["ident"])
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]
         assert r.stdout.strip().splitlines()[-1] == want, (env_val, r.stdout)
+
+
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64, psg.F16, psg.BF16])
+def test_cached_slot_list_served_as_a_stretch(dtype):
+    """psg_store_slots_stretch finds a resolved slot list that is a stretch of
+    the store (slots[i] == first + i) — the whole list, any contiguous part of
+    it — and nothing else (a sparse list, a list with an absent key);
+    psg_store_handle_stretch then serves it without the slot stream, bit-exact
+    against the oracle, at aligned and unaligned first slots and value buffers."""
+    rng, univ, st, orc = populated(dtype, 120000, 67)
+    for lo, hi in [(0, len(univ)), (3, 70003), (4096, 4096 + 8191), (len(univ) - 1, len(univ))]:
+        k = univ[lo:hi]
+        n = len(k)
+        slots = psg.DeviceBuffer(n * 4)
+        st.resolve(dev(k), n, slots, insert=False)
+        first = st.slots_stretch(slots, n)
+        assert first == lo, (lo, hi, first)
+        for off in (0, 4):
+            for r, flags in enumerate([psg.PUSH, ALL, psg.PULL]):
+                v = oracle.synth(n, dtype, 40 * lo + 10 * off + r, 1, -1.0, 1.0)
+                dv = psg.DeviceBuffer(off + n * ES[dtype])
+                out = psg.DeviceBuffer(off + n * ES[dtype])
+                dv.upload(v, offset=off)
+                st.handle_stretch(flags, first, dv.ptr + off if flags & psg.PUSH else None,
+                                  out.ptr + off if flags & psg.PULL else None, n)
+                exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
+                if flags & psg.PULL:
+                    np.testing.assert_array_equal(out.download(NPT[dtype], n, offset=off), exp)
+    same_store(st, orc, dtype)
+    # not stretches: every other key; a key the store lacks (slot UINT32_MAX)
+    k = univ[::2].copy()
+    slots = psg.DeviceBuffer(len(k) * 4)
+    st.resolve(dev(k), len(k), slots, insert=False)
+    assert st.slots_stretch(slots, len(k)) is None
+    k = univ[100:200].copy()
+    k[50] = k[49] + (k[50] - k[49]) // np.uint64(2)
+    slots = psg.DeviceBuffer(len(k) * 4)
+    st.resolve(dev(k), len(k), slots, insert=False)
+    assert st.slots_stretch(slots, len(k)) is None
+    # a stretch past the store is refused
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle_stretch(psg.PULL, len(univ) - 5, None, psg.DeviceBuffer(40), 10)
+    assert ei.value.code == 4
