@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "psg_internal.h"
 
@@ -53,11 +54,21 @@ __device__ __forceinline__ void st_nt(V* p, V x, int nt) {
 // moment pairs instead of two.  Element accessors for feature i:
 __device__ __forceinline__ uint64_t blk_m(uint64_t i) { return (i >> 7) * 256 + (i & 127); }
 __device__ __forceinline__ uint64_t blk_v(uint64_t i) { return (i >> 7) * 256 + 128 + (i & 127); }
+// the m and v of feature i (BLK: the one blocked array m)
+template <bool BLK>
+__device__ __forceinline__ double* mom_m(double* m, uint64_t i) {
+  return BLK ? m + blk_m(i) : m + i;
+}
+template <bool BLK>
+__device__ __forceinline__ double* mom_v(double* m, double* v, uint64_t i) {
+  return BLK ? m + blk_v(i) : v + i;
+}
 
-// MAXG: gradient slots the kernel keeps registers for (4 when ng <= 4: 125 ->
-// fewer VGPRs, more waves in flight; else kMaxGrads).  BLK: the moments in the
-// blocked layout (m is the one array, v unused).
-template <bool ADAM, bool ZERO, int MAXG, bool BLK>
+// MAXG: gradient slots the kernel keeps registers for; EXACT: a round of
+// exactly MAXG frames (1..4: every slot loaded, no run-time frame test, so the
+// registers of absent frames are not held), else up to kMaxGrads (ng at run
+// time).  BLK: the moments in the blocked layout (m is the one array, v unused).
+template <bool ADAM, bool ZERO, int MAXG, bool BLK, bool EXACT>
 __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Grads g, int ng, uint64_t n,
                                                       float lr, double* __restrict__ m,
                                                       double* __restrict__ v, double alr, double b1,
@@ -72,12 +83,12 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
       f32x4 x[MAXG];
 #pragma unroll
       for (int k = 0; k < MAXG; ++k)
-        if (k < ng)
+        if (EXACT || k < ng)
           x[k] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(g.p[k]) + j));
       f32x4 s = ZERO ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} + x[0] : x[0];
 #pragma unroll
       for (int k = 1; k < MAXG; ++k)
-        if (k < ng) s = s + x[k];
+        if (EXACT || k < ng) s = s + x[k];
       f32x4 wv = __builtin_bit_cast(f32x4, ld_nt(reinterpret_cast<const u32x4*>(w + 4 * j), nt));
 #pragma unroll
       for (int e = 0; e < 4; ++e) wv[e] = (float)((double)wv[e] - (double)(lr * s[e]));
@@ -89,61 +100,67 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
     // contiguous run (512 B of f32 pairs, 1 KiB of f64 pairs).  With four
     // consecutive features per lane the f64 moments moved at a 32-B lane
     // stride, each instruction writing half of every line (0.63 of HBM at 64 M
-    // features).
+    // features).  T wave tiles per iteration, every load of the T tiles issued
+    // before the first update: T = 2 for an exact frame count (the in-place
+    // moment read-modify-write is the slow stream, and two tiles keep twice
+    // its lines in flight: tools/probe_adam.hip), 1 for a run-time count (its
+    // registers would halve the waves).
+    constexpr int T = EXACT ? 2 : 1;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const uint64_t nu = vec ? n / 256 * 64 : 0;  // lane units of whole wave tiles
     done = nu * 4;
-    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nu; j += stride) {
-      const uint64_t f0 = (j >> 6) * 256 + 2 * (j & 63);  // first pair; the second is f0 + 128
-      f32x2 x[MAXG][2];
+    for (uint64_t j0 = (uint64_t)blockIdx.x * kBlock * T + threadIdx.x; j0 < nu; j0 += stride * T) {
+      f32x2 x[T][MAXG][2];
+      f32x2 wv[T][2];
+      f64x2 mm[T][2], vv[T][2];
+      uint64_t f0[T];
+      bool in[T];
 #pragma unroll
-      for (int k = 0; k < MAXG; ++k)
-        if (k < ng)
+      for (int t = 0; t < T; ++t) {
+        const uint64_t j = j0 + (uint64_t)t * kBlock;
+        in[t] = j < nu;
+        const uint64_t jj = in[t] ? j : j0;  // a tile past the end repeats the first, unwritten
+        f0[t] = (jj >> 6) * 256 + 2 * (jj & 63);  // first pair; the second is f0 + 128
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            x[k][h] = __builtin_bit_cast(
-                f32x2, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g.p[k] + f0 + 128 * h)));
-      f32x2 wv[2];
-      f64x2 mm[2], vv[2];
-      // the moment pairs of features f0 + 128 h (BLK: group 2T + h of the
-      // blocked array, T = f0 / 256, at lane offset f0 % 128)
-      double* mp[2];
-      double* vp[2];
+        for (int k = 0; k < MAXG; ++k)
+          if (EXACT || k < ng)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if constexpr (BLK) {
-          mp[h] = m + blk_m(f0 + 128 * h);
-          vp[h] = m + blk_v(f0 + 128 * h);
-        } else {
-          mp[h] = m + f0 + 128 * h;
-          vp[h] = v + f0 + 128 * h;
+            for (int h = 0; h < 2; ++h)
+              x[t][k][h] = __builtin_bit_cast(
+                  f32x2, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g.p[k] + f0[t] + 128 * h)));
+        // the moment pairs of features f0 + 128 h (BLK: group 2U + h of the
+        // blocked array, U = f0 / 256, at lane offset f0 % 128)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          wv[t][h] = __builtin_bit_cast(f32x2, ld_nt(reinterpret_cast<const u32x2*>(w + f0[t] + 128 * h), nt));
+          mm[t][h] = ld_nt(reinterpret_cast<const f64x2*>(mom_m<BLK>(m, f0[t] + 128 * h)), nt);
+          vv[t][h] = ld_nt(reinterpret_cast<const f64x2*>(mom_v<BLK>(m, v, f0[t] + 128 * h)), nt);
         }
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        wv[h] = __builtin_bit_cast(f32x2, ld_nt(reinterpret_cast<const u32x2*>(w + f0 + 128 * h), nt));
-        mm[h] = ld_nt(reinterpret_cast<const f64x2*>(mp[h]), nt);
-        vv[h] = ld_nt(reinterpret_cast<const f64x2*>(vp[h]), nt);
-      }
+      for (int t = 0; t < T; ++t) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f32x2 s = ZERO ? f32x2{0.0f, 0.0f} + x[0][h] : x[0][h];
+        for (int h = 0; h < 2; ++h) {
+          f32x2 s = ZERO ? f32x2{0.0f, 0.0f} + x[t][0][h] : x[t][0][h];
 #pragma unroll
-        for (int k = 1; k < MAXG; ++k)
-          if (k < ng) s = s + x[k][h];
+          for (int k = 1; k < MAXG; ++k)
+            if (EXACT || k < ng) s = s + x[t][k][h];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double gr = (double)(lr * s[e]);
-          const double mi = b1 * mm[h][e] + (1.0 - b1) * gr;
-          const double vi = b2 * vv[h][e] + (1.0 - b2) * gr * gr;
-          mm[h][e] = mi;
-          vv[h][e] = vi;
-          wv[h][e] = (float)((double)wv[h][e] - alr * (mi / c1) / (sqrt(vi / c2) + eps));
+          for (int e = 0; e < 2; ++e) {
+            const double gr = (double)(lr * s[e]);
+            const double mi = b1 * mm[t][h][e] + (1.0 - b1) * gr;
+            const double vi = b2 * vv[t][h][e] + (1.0 - b2) * gr * gr;
+            mm[t][h][e] = mi;
+            vv[t][h][e] = vi;
+            wv[t][h][e] = (float)((double)wv[t][h][e] - alr * (mi / c1) / (sqrt(vi / c2) + eps));
+          }
+          if (in[t]) {
+            st_nt(reinterpret_cast<f64x2*>(mom_m<BLK>(m, f0[t] + 128 * h)), mm[t][h], nt);
+            st_nt(reinterpret_cast<f64x2*>(mom_v<BLK>(m, v, f0[t] + 128 * h)), vv[t][h], nt);
+            st_nt(reinterpret_cast<u32x2*>(w + f0[t] + 128 * h), __builtin_bit_cast(u32x2, wv[t][h]), nt);
+          }
         }
-        st_nt(reinterpret_cast<f64x2*>(mp[h]), mm[h], nt);
-        st_nt(reinterpret_cast<f64x2*>(vp[h]), vv[h], nt);
-        st_nt(reinterpret_cast<u32x2*>(w + f0 + 128 * h), __builtin_bit_cast(u32x2, wv[h]), nt);
       }
     }
   }
@@ -213,34 +230,33 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   const int ntm = nt_env >= 0 ? (nt_env ? 1 : 0) : (state_bytes > (512ull << 20) ? 1 : 0);
   const double alr = adam ? adam->lr : 0, b1 = adam ? adam->beta1 : 0, b2 = adam ? adam->beta2 : 0,
                eps = adam ? adam->eps : 0;
-#define PSG_LR_LAUNCH(A, Z, G, B)                                                                     \
-  k_lr_apply_sum<A, Z, G, B><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
-  const bool few = ngrads <= 4;
   const bool blk = adam && adam->blocked;
-  if (adam && from_zero) {
-    if (blk) {
-      if (few) PSG_LR_LAUNCH(true, true, 4, true);
-      else PSG_LR_LAUNCH(true, true, kMaxGrads, true);
-    } else {
-      if (few) PSG_LR_LAUNCH(true, true, 4, false);
-      else PSG_LR_LAUNCH(true, true, kMaxGrads, false);
+  auto go = [&](auto adam_c, auto zero_c, auto blk_c) {
+    constexpr bool A = decltype(adam_c)::value, Z = decltype(zero_c)::value, B = decltype(blk_c)::value;
+#define PSG_LR_LAUNCH(G, X) \
+  k_lr_apply_sum<A, Z, G, B, X><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
+    switch (ngrads) {
+      case 1: PSG_LR_LAUNCH(1, true); break;
+      case 2: PSG_LR_LAUNCH(2, true); break;
+      case 3: PSG_LR_LAUNCH(3, true); break;
+      case 4: PSG_LR_LAUNCH(4, true); break;
+      default: PSG_LR_LAUNCH(kMaxGrads, false); break;
     }
-  } else if (adam) {
-    if (blk) {
-      if (few) PSG_LR_LAUNCH(true, false, 4, true);
-      else PSG_LR_LAUNCH(true, false, kMaxGrads, true);
-    } else {
-      if (few) PSG_LR_LAUNCH(true, false, 4, false);
-      else PSG_LR_LAUNCH(true, false, kMaxGrads, false);
-    }
-  } else if (from_zero) {
-    if (few) PSG_LR_LAUNCH(false, true, 4, false);
-    else PSG_LR_LAUNCH(false, true, kMaxGrads, false);
-  } else {
-    if (few) PSG_LR_LAUNCH(false, false, 4, false);
-    else PSG_LR_LAUNCH(false, false, kMaxGrads, false);
-  }
 #undef PSG_LR_LAUNCH
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (adam && from_zero) {
+    if (blk) go(T_{}, T_{}, T_{});
+    else go(T_{}, T_{}, F_{});
+  } else if (adam) {
+    if (blk) go(T_{}, F_{}, T_{});
+    else go(T_{}, F_{}, F_{});
+  } else if (from_zero) {
+    go(F_{}, T_{}, F_{});
+  } else {
+    go(F_{}, F_{}, F_{});
+  }
   PSG_HIP(hipGetLastError());
   return PSG_OK;
 }
