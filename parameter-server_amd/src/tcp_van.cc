@@ -29,7 +29,11 @@
 #include <netinet/tcp.h>
 #include <signal.h>
 #include <spawn.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -120,6 +124,184 @@ struct SockReader {
     return true;
   }
 };
+
+// ---- shared-memory byte pipe (processes of one host) ---------------------------
+// A connection between two processes of one host carries its message bytes
+// through a single-producer single-consumer ring in shared memory instead of
+// the socket: a request round trip crosses two connections, and a loopback
+// TCP hop (two system calls and the stack) costs more than the rest of a small
+// request.  The socket stays open beside it: its first bytes name the ring
+// (kHello), a reader that found the ring empty for PS_SPIN_US blocks in poll()
+// on the socket and the writer rings it (one doorbell byte) only then, and the
+// socket's close is how either side learns the other is gone.  PS_SHM_RING=0
+// keeps every byte on the socket.
+constexpr uint32_t kHello = 0x48475350;  // "PSGH": first bytes of a connection
+constexpr uint64_t kRingBytes = 1 << 20;
+
+struct RingHdr {
+  std::atomic<uint64_t> head;  // bytes written (writer)
+  char pad0[56];
+  std::atomic<uint64_t> tail;  // bytes read (reader)
+  char pad1[56];
+  std::atomic<uint32_t> sleeping;  // the reader waits on the socket for a doorbell
+  char pad2[60];
+  uint64_t cap;
+};
+constexpr size_t kRingHdrBytes = 4096;
+
+bool PeerGone(int fd) {  // the peer closed a connection it never writes to
+  char c;
+  const ssize_t r = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+  return r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR);
+}
+
+struct Ring {
+  RingHdr* h = nullptr;
+  char* data = nullptr;
+  size_t map_bytes = 0;
+  std::string name;
+  bool owner = false;
+  ~Ring() {
+    if (h) ::munmap(h, map_bytes);
+    if (owner) ::shm_unlink(name.c_str());  // (gone already once the reader mapped it)
+  }
+  static std::unique_ptr<Ring> Map(const std::string& name, bool create) {
+    const int fd = ::shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+    if (fd < 0) return nullptr;
+    const size_t bytes = kRingHdrBytes + kRingBytes;
+    if (create && ::ftruncate(fd, (off_t)bytes) != 0) {
+      ::close(fd);
+      ::shm_unlink(name.c_str());
+      return nullptr;
+    }
+    struct stat st;
+    if (::fstat(fd, &st) != 0 || (size_t)st.st_size != bytes) {
+      ::close(fd);
+      if (create) ::shm_unlink(name.c_str());
+      return nullptr;
+    }
+    void* p = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (p == MAP_FAILED) {
+      if (create) ::shm_unlink(name.c_str());
+      return nullptr;
+    }
+    auto r = std::make_unique<Ring>();
+    r->h = static_cast<RingHdr*>(p);
+    r->data = static_cast<char*>(p) + kRingHdrBytes;
+    r->map_bytes = bytes;
+    r->name = name;
+    r->owner = create;
+    if (create) {
+      new (&r->h->head) std::atomic<uint64_t>(0);
+      new (&r->h->tail) std::atomic<uint64_t>(0);
+      new (&r->h->sleeping) std::atomic<uint32_t>(0);
+      r->h->cap = kRingBytes;
+    } else {
+      ::shm_unlink(name.c_str());  // both sides hold it now: nothing left to clean up
+    }
+    return r;
+  }
+  // writer (under the connection's mutex): false once the peer is gone
+  bool Write(int fd, const void* buf, size_t n) {
+    const char* p = static_cast<const char*>(buf);
+    const uint64_t cap = h->cap;
+    while (n) {
+      const uint64_t hd = h->head.load(std::memory_order_relaxed);
+      const uint64_t room = cap - (hd - h->tail.load(std::memory_order_acquire));
+      if (room == 0) {
+        if (!WaitRoom(fd)) return false;
+        continue;
+      }
+      const size_t k = (size_t)std::min<uint64_t>(n, room);
+      const size_t off = (size_t)(hd % cap), first = std::min(k, (size_t)cap - off);
+      std::memcpy(data + off, p, first);
+      std::memcpy(data, p + first, k - first);
+      h->head.store(hd + k, std::memory_order_seq_cst);
+      if (h->sleeping.load(std::memory_order_seq_cst)) {
+        const char bell = 0;
+        const ssize_t w = ::send(fd, &bell, 1, MSG_NOSIGNAL | MSG_DONTWAIT);
+        if (w < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return false;
+      }
+      p += k;
+      n -= k;
+    }
+    return true;
+  }
+  bool WaitRoom(int fd) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0;; ++i) {
+      if (h->head.load(std::memory_order_relaxed) - h->tail.load(std::memory_order_acquire) < h->cap) return true;
+      if (i < 256) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      if (cluster::Aborted() || ((i & 63) == 0 && PeerGone(fd))) return false;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+  // reader: n bytes, waiting as long as the peer lives; false once it closed
+  // the socket with nothing left in the ring
+  bool Read(int fd, void* out, size_t n) {
+    char* p = static_cast<char*>(out);
+    const uint64_t cap = h->cap;
+    while (n) {
+      const uint64_t tl = h->tail.load(std::memory_order_relaxed);
+      const uint64_t avail = h->head.load(std::memory_order_acquire) - tl;
+      if (avail == 0) {
+        if (!WaitData(fd)) return false;
+        continue;
+      }
+      const size_t k = (size_t)std::min<uint64_t>(n, avail);
+      const size_t off = (size_t)(tl % cap), first = std::min(k, (size_t)cap - off);
+      std::memcpy(p, data + off, first);
+      std::memcpy(p + first, data, k - first);
+      h->tail.store(tl + k, std::memory_order_release);
+      p += k;
+      n -= k;
+    }
+    return true;
+  }
+  bool has_data() const {
+    return h->head.load(std::memory_order_acquire) != h->tail.load(std::memory_order_relaxed);
+  }
+  bool WaitData(int fd) {
+    const int us = SpinMicros();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; us > 0; ++i) {
+      if (has_data()) return true;
+      if ((i & 7) == 7 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us)) break;
+      __builtin_ia32_pause();
+    }
+    while (true) {
+      h->sleeping.store(1, std::memory_order_seq_cst);
+      if (h->head.load(std::memory_order_seq_cst) != h->tail.load(std::memory_order_relaxed)) {
+        h->sleeping.store(0, std::memory_order_relaxed);
+        return true;
+      }
+      pollfd pfd{fd, POLLIN, 0};
+      const int pr = ::poll(&pfd, 1, 100);
+      h->sleeping.store(0, std::memory_order_relaxed);
+      if (pr < 0 && errno != EINTR) return has_data();
+      if (pr > 0) {
+        char bells[256];
+        const ssize_t r = ::recv(fd, bells, sizeof(bells), MSG_DONTWAIT);
+        if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR))
+          return has_data();  // closed: what is left in the ring is still read
+      }
+      if (has_data()) return true;
+    }
+  }
+};
+
+bool RingEnabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_SHM_RING");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 
 // Before a connection's reader blocks in recv for the next message, poll the
 // socket for up to PS_SPIN_US (default 50 us, the spin of the request queues,
@@ -338,8 +520,11 @@ struct FrameRegistry {
 
 struct Conn {
   int fd = -1;
-  std::mutex mu;  // one writer at a time
+  std::mutex mu;               // one writer at a time
+  std::unique_ptr<Ring> ring;  // the message bytes' path when the peer shares this host
+  bool Put(const void* p, size_t n) { return ring ? ring->Write(fd, p, n) : WriteAll(fd, p, n); }
   ~Conn() {
+    ring.reset();
     if (fd >= 0) ::close(fd);
   }
 };
@@ -748,6 +933,18 @@ std::shared_ptr<Conn> TcpVan::Connect(int id) {
   Tune(fd);
   auto c = std::make_shared<Conn>();
   c->fd = fd;
+  // the connection's first bytes: kHello and the name of its ring (empty: the
+  // socket carries everything)
+  std::string name;
+  if (RingEnabled() && n.hostname == my_node_.hostname) {
+    static std::atomic<uint64_t> seq{0};
+    name = "/psgring." + std::to_string(::getpid()) + "." + std::to_string(my_node_.id) + "." + std::to_string(id) +
+           "." + std::to_string(seq++);
+    c->ring = Ring::Map(name, true);
+    if (!c->ring) name.clear();
+  }
+  const uint32_t hello[2] = {kHello, (uint32_t)name.size()};
+  if (!WriteAll(fd, hello, sizeof(hello)) || (name.size() && !WriteAll(fd, name.data(), name.size()))) return nullptr;
   std::lock_guard<std::mutex> lk(peers_mu_);
   auto ins = conns_.emplace(id, c);
   return ins.first->second;  // a racing connect to the same peer: keep one
@@ -846,9 +1043,9 @@ int TcpVan::SendMsg(const Message& msg) {
   const int bytes = Encode(msg, dst, &head, &host);
   std::lock_guard<std::mutex> lk(c->mu);
   // frame descriptors precede the host frame payloads, in frame order
-  if (!WriteAll(c->fd, head.data(), head.size())) return -1;
+  if (!c->Put(head.data(), head.size())) return -1;
   for (const SVector<char>& h : host)
-    if (h.size() && !WriteAll(c->fd, h.data(), h.size())) return -1;
+    if (h.size() && !c->Put(h.data(), h.size())) return -1;
   return bytes;
 }
 
@@ -890,12 +1087,39 @@ SVector<char> TcpVan::MapShmFrame(int sender, const ShmFrame& f, uint64_t bytes)
 }
 
 void TcpVan::ReadLoop(int fd) {
-  SockReader rd(fd);
+  SockReader sock(fd);
+  // the connection's hello: the name of the writer's ring, if any
+  std::unique_ptr<Ring> ring;
+  {
+    uint32_t hello[2];
+    if (!sock.read(hello, sizeof(hello)) || hello[0] != kHello || hello[1] > 255) {
+      LOG(ERROR) << "connection without a hello; closing it";
+      return;
+    }
+    if (hello[1]) {
+      std::string name(hello[1], '\0');
+      if (!sock.read(&name[0], name.size())) return;
+      ring = Ring::Map(name, false);
+      if (!ring) {
+        // the losing side of two racing connects to one peer (Connect keeps
+        // one; the other's ring is gone with it), or a ring this process cannot
+        // map: close the connection, so a writer still using it fails loudly
+        ::shutdown(fd, SHUT_RDWR);
+        return;
+      }
+    }
+  }
+  struct Source {
+    SockReader& sock;
+    Ring* ring;
+    int fd;
+    bool read(void* out, size_t n) { return ring ? ring->Read(fd, out, n) : sock.read(out, n); }
+  } rd{sock, ring.get(), fd};
   int peer = Node::kEmpty;
   bool said_goodbye = false;
   while (true) {
     WireHeader wh;
-    if (rd.empty()) SpinUntilReadable(fd);
+    if (!ring && sock.empty()) SpinUntilReadable(fd);
     if (!rd.read(&wh, sizeof(wh))) break;
     if (wh.magic != kMagic) {
       LOG(ERROR) << "bad frame header from node " << peer << "; closing the connection";
@@ -1053,7 +1277,7 @@ void TcpVan::Stop() {
     std::vector<SVector<char>> host;
     Encode(bye, Node(), &head, &host);
     std::lock_guard<std::mutex> lk(kv.second->mu);
-    WriteAll(kv.second->fd, head.data(), head.size());
+    kv.second->Put(head.data(), head.size());
     ::shutdown(kv.second->fd, SHUT_RDWR);
   }
   if (listen_fd_ >= 0) {

@@ -221,3 +221,29 @@ def test_process_mode_host_frames_travel_as_shared_memory():
     assert stats[9][1] > 0 and stats[11][1] > 0, stats  # workers' Push frames
     assert stats[8][0] > 0 and stats[10][0] > 0, stats  # servers echo the keys back
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("psg.")]
+
+
+@pytest.mark.parametrize("ring", ["1", "0"])
+def test_process_mode_message_ring(ring):
+    """Process mode carries each connection's message bytes through a shared-
+    memory ring (PS_SHM_RING=1, the default on one host) or the socket (0).
+    Both run the host cluster harness with large requests whose host frames
+    stay inline (PS_SHM_FRAMES=0: 300 000 keys, 2.4 MB a frame, several times
+    the 1 MiB ring, so the writer waits for room as the reader drains), and the
+    request round trip of the latency harness; no ring is left in /dev/shm."""
+    import json
+    exe = os.path.join(BIN, "kv_cluster_host")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 2, "-procs", 300000, env={"PS_SHM_RING": ring, "PS_SHM_FRAMES": "0"},
+            timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count(" ok") == 2
+    lat = os.path.join(BIN, "kv_latency_host")
+    _need(lat)
+    r = run(lat, "-ns", 1, "-nw", 1, "-procs",
+            env={"PS_SHM_RING": ring, "LAT_ITERS": "5000", "LAT_MODE": "ring" + ring}, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["iters"] == 5000 and line["us_per_request"] > 0
+    print(line)
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("psgring.")]
