@@ -25,9 +25,19 @@ int main(int argc, char* argv[]) {
   const char* em = std::getenv("LAT_MODE");
   const long iters = ei ? std::atol(ei) : 20000;
   const long nkeys = ek ? std::atol(ek) : 1;
+  // LAT_WORK_US: the handle busy-waits this long first (a request's device
+  // time, e.g. ~50 us for a 10 M-key keyed Push), so the waiting threads of the
+  // worker outlast their spin as they do behind a real request
+  const char* ew = std::getenv("LAT_WORK_US");
+  const long work_us = ew ? std::atol(ew) : 0;
   if (IsServer()) {
     auto server = new KVServer<float>(0);
-    server->SetRequestHandle([](const KVMeta& meta, const KVPairs<float>& req, KVServer<float>* s) {
+    server->SetRequestHandle([work_us](const KVMeta& meta, const KVPairs<float>& req, KVServer<float>* s) {
+      if (work_us > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(work_us)) {
+        }
+      }
       KVPairs<float> res;
       if (meta.pull) {
         res.keys = req.keys;
@@ -51,8 +61,8 @@ int main(int argc, char* argv[]) {
       us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count() / (double)(iters / 5));
     }
     std::sort(us.begin(), us.end());
-    printf("{\"mode\": \"%s\", \"iters\": %ld, \"keys\": %ld, \"us_per_request\": %.2f, \"min\": %.2f, \"max\": %.2f}\n",
-           em ? em : "?", iters, nkeys, us[us.size() / 2], us.front(), us.back());
+    printf("{\"mode\": \"%s\", \"iters\": %ld, \"keys\": %ld, \"work_us\": %ld, \"us_per_request\": %.2f, \"min\": %.2f, \"max\": %.2f}\n",
+           em ? em : "?", iters, nkeys, work_us, us[us.size() / 2], us.front(), us.back());
     fflush(stdout);
   }
   Finalize(0, true);
