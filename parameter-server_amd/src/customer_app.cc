@@ -33,7 +33,7 @@ int Customer::NewRequest(int receiver) {
 int SpinMicros() {
   static const int us = [] {
     const char* e = std::getenv("PS_SPIN_US");
-    return e ? std::atoi(e) : 50;
+    return e ? std::atoi(e) : 250;
   }();
   return us;
 }

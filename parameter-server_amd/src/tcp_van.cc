@@ -304,7 +304,7 @@ bool RingEnabled() {
 }
 
 // Before a connection's reader blocks in recv for the next message, poll the
-// socket for up to PS_SPIN_US (default 50 us, the spin of the request queues,
+// socket for up to PS_SPIN_US (default 250 us, the spin of the request queues,
 // internal/customer.h): a request round trip crosses the socket twice, and a
 // blocked reader's wake-up costs more than a loopback hop.
 void SpinUntilReadable(int fd) {
