@@ -234,8 +234,8 @@ int psg_store_wait(psg_store* s, uint64_t ticket);
 
 /* The stable device radix sort of the order-preserving path (psg_sort.hip),
  * exported for its parity tests: sorts (keys[i], vals[i]) by bits [0, bits) of
- * the key, equal keys keeping their order.  In place; synchronous on `stream`'s
- * order (allocates its scratch stream-ordered). */
+ * the key, equal keys keeping their order.  In place; synchronises `stream`
+ * (its scratch is allocated before and freed after). */
 int psg_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t n, int bits, psg_stream stream);
 
 /* Slot cache (LR USE_KEY_CACHING, tests/src/LRServer.h:127-142): resolve a key

@@ -241,20 +241,35 @@ int psg_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t n, int bits, psg
   PSG_REQUIRE(bits >= 1 && bits <= 64, PSG_ERR_INVALID, "psg_sort_pairs_u64: bits %d", bits);
   if (n == 0) return PSG_OK;
   hipStream_t st = (hipStream_t)stream;
+  // scratch by plain allocations, freed once the stream has finished with
+  // them: one intermittent wrong result of this export (vals half unwritten,
+  // n = 17) came from a run whose scratch was stream-ordered on the legacy
+  // null stream (hipMallocAsync / hipFreeAsync), the only thing about it no
+  // other sort in the library shares
   uint64_t* ka = nullptr;
   uint32_t *va = nullptr, *counts = nullptr;
-  PSG_HIP(hipMallocAsync((void**)&ka, n * sizeof(uint64_t), st));
-  PSG_HIP(hipMallocAsync((void**)&va, n * sizeof(uint32_t), st));
-  PSG_HIP(hipMallocAsync((void**)&counts, radix_counts_elems(n) * sizeof(uint32_t), st));
-  int res = 0;
-  int rc = radix_sort_u64(keys, vals, n, bits, false, ka, va, counts, st, &res);
-  if (rc == PSG_OK && res == 1) {
-    PSG_HIP(hipMemcpyAsync(keys, ka, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
-    PSG_HIP(hipMemcpyAsync(vals, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  int rc = PSG_OK;
+  auto release = [&] {
+    if (ka) (void)hipFree(ka);
+    if (va) (void)hipFree(va);
+    if (counts) (void)hipFree(counts);
+  };
+  if (hipMalloc((void**)&ka, n * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc((void**)&va, n * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&counts, radix_counts_elems(n) * sizeof(uint32_t)) != hipSuccess) {
+    release();
+    return hip_fail(hipErrorOutOfMemory, "psg_sort_pairs_u64 scratch", __FILE__, __LINE__);
   }
-  (void)hipFreeAsync(ka, st);
-  (void)hipFreeAsync(va, st);
-  (void)hipFreeAsync(counts, st);
+  int res = 0;
+  rc = radix_sort_u64(keys, vals, n, bits, false, ka, va, counts, st, &res);
+  if (rc == PSG_OK && res == 1) {
+    if (hipMemcpyAsync(keys, ka, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(vals, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+      rc = hip_fail(hipGetLastError(), "psg_sort_pairs_u64 copy back", __FILE__, __LINE__);
+  }
+  const hipError_t se = hipStreamSynchronize(st);
+  if (rc == PSG_OK && se != hipSuccess) rc = hip_fail(se, "psg_sort_pairs_u64 sync", __FILE__, __LINE__);
+  release();
   return rc;
 }
 
