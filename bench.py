@@ -655,6 +655,20 @@ class GpuBackend:
         b2b_ms = statistics.median(eb[i].elapsed_ms(eb[i + 1]) for i in range(iters))
         bad, _ = p.verify_synth_sum(o, n, p.F32, self._seed, 1, 0.0, 1000.0, float(warm + iters),
                                     stream=self.stream)  # the last Pull, before the b2b Pushes
+        # this box's own copy ceiling: the runtime's device-to-device copy of
+        # the same 1 GiB (read + write), so a kernel's fraction can be read
+        # against what this GPU's HBM and page placement give a plain copy
+        # (MI355X_MICROARCH.md quotes 6.29 TB/s from one box; boxes differ)
+        self.sync()
+        ec = [p.Event() for _ in range(11)]
+        for _ in range(2):
+            p.memcpy_d2d(o, v, n * 4, stream=self.stream)
+        ec[0].record(self.stream)
+        for i in range(10):
+            p.memcpy_d2d(o, v, n * 4, stream=self.stream)
+            ec[i + 1].record(self.stream)
+        self.sync()
+        copy_ms = statistics.median(ec[i].elapsed_ms(ec[i + 1]) for i in range(10))
         st.close()
         v.free()
         o.free()
@@ -665,6 +679,12 @@ class GpuBackend:
             out[f"{name}_achieved"] = round(gbs, 1)
             out[f"{name}_frac"] = round(gbs / HBM_PEAK_GBS, 4)
         out["push_back_to_back_frac"] = round(PUSH_ACCESSES * 4 * n / (b2b_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        copy_gbs = 2 * 4 * n / (copy_ms * 1e-3) / 1e9
+        out["copy_ceiling"] = {"what": "hipMemcpyAsync device-to-device of the same 1 GiB, read + write bytes",
+                               "ms": round(copy_ms, 5), "achieved": round(copy_gbs, 1),
+                               "frac": round(copy_gbs / HBM_PEAK_GBS, 4),
+                               "push_of_copy": round(out["push_achieved"] / copy_gbs, 4),
+                               "pull_of_copy": round(out["pull_achieved"] / copy_gbs, 4)}
         out["kernel"] = "k_dense_vec<PUSH> / <PULL>, 12 / 8 B per float"
         return out
 

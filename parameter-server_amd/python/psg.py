@@ -300,6 +300,11 @@ class DeviceBuffer:
             pass
 
 
+def memcpy_d2d(dst, src, nbytes: int, stream=None) -> None:
+    """Device-to-device copy (psg_memcpy, kind 2), stream-ordered."""
+    _call("psg_memcpy", C.c_void_p(_ptr(dst)), C.c_void_p(_ptr(src)), nbytes, 2, _s(stream))
+
+
 def checksum(ptr, nbytes: int, stream=None) -> int:
     """psg_checksum of a device range (synchronises the stream)."""
     h = C.c_uint64(0)
