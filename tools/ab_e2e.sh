@@ -11,7 +11,7 @@ for r in $(seq 1 "$R"); do
       env $e timeout -k 10 120 tests/_bin/kv_cluster_device -ns 1 -nw 1 $mode 10000000 20 > gpurun_out/ab_e2e.log 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "$e $mode rc=$rc"; tail -3 gpurun_out/ab_e2e.log; exit $rc; fi
-      printf "%-22s %-7s %s\n" "$e" "${mode:-thr}" "$(grep '^{' gpurun_out/ab_e2e.log | head -1 | cut -c1-160)"
+      printf "%-22s %-7s %s\n" "$e" "${mode:-thr}" "$(grep '^{' gpurun_out/ab_e2e.log | head -1 | cut -c40-240)"
     done
   done
 done
