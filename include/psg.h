@@ -262,6 +262,14 @@ int psg_store_slots_stretch(psg_store* s, const uint32_t* slots, uint64_t n, uin
                             psg_stream stream);
 int psg_store_handle_stretch(psg_store* s, int flags, uint64_t first, const void* vals, void* out,
                              uint64_t n, psg_stream stream);
+/* Return once everything enqueued on `stream` so far has run (a slot or
+ * stretch request's values no longer read, its Pull reply in memory): the
+ * stream writes a word into the store's pinned memory behind that work and
+ * the caller spins on it — what psg_store_handle does for its own requests —
+ * instead of a runtime stream wait; after 2 ms it falls back to one
+ * (PSG_SYNC_POLL=0: always).  Lets a server answer a cached-list request as
+ * soon as its kernel ends (KVServer::Response, KVApp.h:466-478). */
+int psg_store_sync(psg_store* s, psg_stream stream);
 
 /* The hash a key list is cached under in LR key caching (the std::hash
  * specialisation of tests/src/LRServer.h:11-29, which LRWorker.h:214-219 also

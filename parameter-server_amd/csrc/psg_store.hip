@@ -2236,6 +2236,12 @@ int psg_store_handle_stretch(psg_store* s, int flags, uint64_t first, const void
                        (hipStream_t)stream);
 }
 
+int psg_store_sync(psg_store* s, psg_stream stream) {
+  PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_sync: null store");
+  PSG_TRY(drain(s));
+  return read_flags(s, (hipStream_t)stream);
+}
+
 int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots, const void* vals,
                            void* out, uint64_t n, psg_stream stream) {
   PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_handle_slots: null store");

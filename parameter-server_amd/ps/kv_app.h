@@ -438,7 +438,8 @@ struct KVServerDefaultHandle {
       else
         device::Check(psg_store_handle_slots(state->store, flags, c.slots.data(), dvals.data(), dout.data(), n, s),
                       "psg_store_handle_slots");
-      device::Check(psg_stream_sync(s), "psg_stream_sync");
+      // answered once the kernel has ended: a polled word, not a stream wait
+      device::Check(psg_store_sync(state->store, s), "psg_store_sync");
     } else if (n && flags) {
       if (req_meta.push) CHECK_EQ(n, req_data.vals.size());
       SVector<Key> dkeys = detail::ToDeviceAsync(req_data.keys, dev);

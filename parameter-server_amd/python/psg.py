@@ -42,7 +42,7 @@ EXPORTS = [
     "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear", "psg_store_counters",
     "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots",
-    "psg_store_slots_stretch", "psg_store_handle_stretch", "psg_store_dump",
+    "psg_store_slots_stretch", "psg_store_handle_stretch", "psg_store_sync", "psg_store_dump",
     "psg_key_list_hash",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
@@ -120,6 +120,7 @@ def lib() -> C.CDLL:
             "psg_store_handle_slots": ([vp, i32, vp, vp, vp, u64, vp], i32),
             "psg_store_slots_stretch": ([vp, vp, u64, C.POINTER(u64), vp], i32),
             "psg_store_handle_stretch": ([vp, i32, u64, vp, vp, u64, vp], i32),
+            "psg_store_sync": ([vp, vp], i32),
             "psg_store_dump": ([vp, vp, vp], i32),
             "psg_key_list_hash": ([vp, u64, C.POINTER(u64), vp], i32),
             "psg_server_ranges": ([i32, vp, vp], i32),
@@ -392,6 +393,11 @@ class Store:
 
     def handle_stretch(self, flags: int, first: int, vals, out, n: int, stream=None) -> None:
         _call("psg_store_handle_stretch", self.h, flags, first, _ptr(vals), _ptr(out), n, _s(stream))
+
+    def sync(self, stream=None) -> None:
+        """Wait for the stream's enqueued work through the store's polled word
+        (psg_store_sync)."""
+        _call("psg_store_sync", self.h, _s(stream))
 
     def clear(self, stream=None) -> None:
         _call("psg_store_clear", self.h, _s(stream))

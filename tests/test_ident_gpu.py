@@ -274,3 +274,41 @@ def test_cached_slot_list_served_as_a_stretch(dtype):
     with pytest.raises(psg.PsgError) as ei:
         st.handle_stretch(psg.PULL, len(univ) - 5, None, psg.DeviceBuffer(40), 10)
     assert ei.value.code == 4
+
+
+def test_store_sync_returns_with_the_reply_in_memory():
+    """psg_store_sync: after a stretch Pull into pinned host memory on a user
+    stream, the reply is readable as soon as the call returns (no other wait);
+    with keyed requests in flight it reaps them first; with nothing enqueued
+    it returns at once."""
+    import ctypes as C
+    rng, univ, st, orc = populated(psg.F32, 200000, 71)
+    n = len(univ)
+    slots = psg.DeviceBuffer(n * 4)
+    st.resolve(dev(univ), n, slots, insert=False)
+    first = st.slots_stretch(slots, n)
+    assert first == 0
+    s = psg.Stream()
+    host = C.c_void_p(None)
+    psg._call("psg_host_alloc", C.byref(host), C.c_size_t(n * 4))
+    try:
+        view = np.ctypeslib.as_array((C.c_float * n).from_address(host.value))
+        st.sync(s)  # nothing enqueued
+        for r in range(3):
+            v = oracle.synth(n, psg.F32, 900 + r, 1, -1.0, 1.0)
+            dv = dev(v)
+            view[:] = np.nan
+            st.handle_stretch(ALL, first, dv, host.value, n, s)
+            st.sync(s)
+            exp = orc.handle(ALL, univ, v, n)
+            np.testing.assert_array_equal(view, exp)
+        # a keyed request in flight on another stream is reaped first
+        v = oracle.synth(n, psg.F32, 950, 1, -1.0, 1.0)
+        dk, dv = dev(univ), dev(v)  # held until the request is reaped
+        st.handle_async(psg.PUSH, dk, dv, None, n)
+        orc.handle(psg.PUSH, univ, v, n)
+        st.sync(s)
+        same_store(st, orc, psg.F32)
+    finally:
+        psg._call("psg_host_free", host)
+        s.close()
