@@ -107,7 +107,7 @@ struct KVServerLRHandle {
       res.keys = req.keys;
       auto dout = SVector<float>::OnDevice(n, PostOffice::Get()->device());
       device::Check(psg_store_handle(s.weights, PSG_PULL, nullptr, 0, nullptr, dout.data(), n, strm), "pull");
-      device::Check(psg_stream_sync(strm), "psg_stream_sync");
+      device::Check(psg_store_sync(s.weights, strm), "psg_store_sync");  // the reply in memory
       res.vals = req.keys.on_device() ? dout : detail::ToHost(dout);
       server->Response(meta, res);
     }
@@ -149,7 +149,7 @@ struct KVServerLRHandle {
     if (!s.folded) device::Check(psg_store_clear(s.fold, strm), "psg_store_clear");
     for (const auto& g : s.grads)
       device::Check(psg_store_handle(s.fold, PSG_PUSH, nullptr, 0, g.data(), nullptr, s.n, strm), "fold push");
-    device::Check(psg_stream_sync(strm), "psg_stream_sync");
+    device::Check(psg_store_sync(s.fold, strm), "psg_store_sync");
     s.grads.clear();
     s.folded = true;
   }
@@ -165,7 +165,7 @@ struct KVServerLRHandle {
     device::Check(psg_lr_apply_sum(s.weights, g.data(), (int)g.size(), from_zero && !s.folded ? 1 : 0, s.n,
                                    s.lr, s.adam, s.iteration, strm),
                   "psg_lr_apply_sum");
-    device::Check(psg_stream_sync(strm), "psg_stream_sync");  // frames are released below
+    device::Check(psg_store_sync(s.weights, strm), "psg_store_sync");  // frames are released below
     s.grads.clear();
     s.folded = false;
   }
