@@ -245,7 +245,19 @@ static DenseCfg dense_cfg_for(uint64_t store_bytes, int op) {
 static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op) {
   DenseCfg c = dense_cfg();
   if (c.nt >= 0) return c;  // explicit sweep settings
-  if (store_bytes <= (512ull << 20)) {
+  if (store_bytes <= (64ull << 20)) {
+    // a request of at most 64 MiB (a 10 M-key cached stretch, an LR model):
+    // 1 vector per lane at 8 blocks/CU — more waves in flight over the short
+    // launch's ramp and tail.  10 M floats Push+Pull, 4 interleaved rounds:
+    // 2,454-2,517 GB/s against 2,419-2,435 at 2 x 2/CU
+    // (profiles/r3_ab_dense_shape_10M.txt)
+    // (PSG_DENSE_UNROLL / PSG_DENSE_BPC, when set, still win: A/B runs)
+    static const bool env_u = getenv("PSG_DENSE_UNROLL") != nullptr;
+    static const bool env_b = getenv("PSG_DENSE_BPC") != nullptr;
+    c.nt = 1;
+    if (!env_u) c.unroll = 1;
+    if (!env_b) c.blocks_per_cu = 8;
+  } else if (store_bytes <= (512ull << 20)) {
     c.nt = 1;
   } else {
     // past the Infinity Cache, all non-temporal.  Pull (the Pull-only sweep
