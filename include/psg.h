@@ -203,8 +203,8 @@ int psg_store_counters(psg_store* s, uint64_t* out, int n);
  * store writes may still be in flight: work that reads the store must be
  * ordered after it on `stream`.  (On the steady SORTED path it waits for the
  * completion word its own kernel writes, which also carries the request's
- * flags, and for a Pull for a pinned word the stream writes behind the kernel
- * — not for the stream itself.)  The store
+ * flags, and for a Pull for an event recorded behind the kernel, polled —
+ * not for the stream itself.)  The store
  * remembers the LDS windows of the last few key arrays it saw (by device
  * pointer and n) and verifies them per tile, so a caller may rewrite a key
  * array in place between requests. */
@@ -262,13 +262,15 @@ int psg_store_slots_stretch(psg_store* s, const uint32_t* slots, uint64_t n, uin
                             psg_stream stream);
 int psg_store_handle_stretch(psg_store* s, int flags, uint64_t first, const void* vals, void* out,
                              uint64_t n, psg_stream stream);
-/* Return once everything enqueued on `stream` so far has run (a slot or
- * stretch request's values no longer read, its Pull reply in memory): the
- * stream writes a word into the store's pinned memory behind that work and
- * the caller spins on it — what psg_store_handle does for its own requests —
- * instead of a runtime stream wait; after 2 ms it falls back to one
- * (PSG_SYNC_POLL=0: always).  Lets a server answer a cached-list request as
- * soon as its kernel ends (KVServer::Response, KVApp.h:466-478). */
+/* Return once everything enqueued on `stream` so far has run, its writes
+ * visible to any agent (a slot or stretch request's values no longer read, its
+ * Pull reply in memory for a copy engine, the host or another process): an
+ * event recorded behind that work and polled with hipEventQuery — what
+ * psg_store_handle does for its own Pull replies — instead of a sleeping
+ * stream wait; after 2 ms it falls back to hipEventSynchronize
+ * (PSG_SYNC_POLL=0: hipStreamSynchronize always).  Lets a server answer a
+ * cached-list request as soon as its kernel ends (KVServer::Response,
+ * KVApp.h:491-513). */
 int psg_store_sync(psg_store* s, psg_stream stream);
 
 /* The hash a key list is cached under in LR key caching (the std::hash

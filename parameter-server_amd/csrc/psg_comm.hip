@@ -216,8 +216,9 @@ int psg_comm_destroy(psg_comm* c) {
 int psg_comm_sync(psg_comm* c, psg_stream stream, double timeout_s) {
   PSG_REQUIRE(c, PSG_ERR_INVALID, "psg_comm_sync: null comm");
   PSG_REQUIRE(!c->aborted, PSG_ERR_COMM, "psg_comm_sync: the communicators were aborted");
+  const double limit_s = timeout_s > 0 ? timeout_s : comm_timeout_s();  // 0: the default
   const auto deadline = std::chrono::steady_clock::now() +
-                        std::chrono::microseconds((int64_t)((timeout_s > 0 ? timeout_s : comm_timeout_s()) * 1e6));
+                        std::chrono::microseconds((int64_t)(limit_s * 1e6));
   hipStream_t sts[2] = {(hipStream_t)stream, c->side};
   for (hipStream_t st : sts) {
     for (;;) {
@@ -232,7 +233,7 @@ int psg_comm_sync(psg_comm* c, psg_stream stream, double timeout_s) {
           if (c->comm[k]) (void)ncclCommAbort(c->comm[k]);
         for (int k = 0; k < kCommIds; ++k) c->comm[k] = nullptr;
         c->aborted = true;
-        set_error("psg_comm_sync: the collectives did not complete within %.0f s; communicators aborted", timeout_s);
+        set_error("psg_comm_sync: the collectives did not complete within %.0f s; communicators aborted", limit_s);
         return PSG_ERR_COMM;
       }
       std::this_thread::sleep_for(std::chrono::microseconds(100));

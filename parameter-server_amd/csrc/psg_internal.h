@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <deque>
 #include <string>
+#include <vector>
 
 #include "../../include/psg.h"
 
@@ -149,7 +150,7 @@ struct InflightReq {
   int wc;         // window-cache entry it ran on
   hipStream_t stream;
   int want_land;  // a Pull answered when reaped (psg_store_handle): its reply must be in memory then
-  int land;       // ... and the stream writes tag to ring_host[kRing + ring] after the kernel to say so
+  int land;       // ... and land_ev[ring] was recorded behind its kernels to say so
   int ident;      // sent as an identity request (k_ident_check / k_ident_apply)
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
@@ -179,7 +180,10 @@ struct psg_store {
   // host has done an earlier request's follow-up (insert, out-of-order path).
   int* reject_dev;
   int seq;           // request sequence number (never 0 after the first request)
-  uint32_t done_seq; // completion words the stream has been asked to write (read_flags)
+  // completion events (psg_store.hip, stream_done / wait_landed): one for the
+  // host's waits on a stream, one per ring slot for a synchronous Pull's reply
+  hipEvent_t done_ev;
+  hipEvent_t land_ev[psg::kRing];
   // k_resolve_apply's arrival counters, one set per ring slot: 8 shard
   // counters and a top counter, 64-bit, each on its own 256 B; zeroed by the
   // block that completes the request
@@ -188,7 +192,7 @@ struct psg_store {
   // kernel with one system-scope store (pinned host memory, kRing words)
   uint32_t* ring_host;
   uint32_t* ring_dev;
-  hipStream_t unlanded;  // a stream whose reaped async Pulls psg_store_wait still synchronises
+  std::vector<hipStream_t> unlanded;  // streams whose reaped async Pulls psg_store_wait still synchronises
   uint32_t ring_next;
   uint32_t tag;
   // fused requests in flight, in launch (= stream) order

@@ -295,6 +295,9 @@ int psg_adam_create(uint64_t n, double learning_rate, double beta1, double beta2
     if (e == hipSuccess) e = hipMemset(a->m, 0, n * sizeof(double));
     if (e == hipSuccess) e = hipMemset(a->v, 0, n * sizeof(double));
   }
+  // null-stream memsets: done before the caller's (non-blocking) streams use
+  // the moments
+  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
   if (e != hipSuccess) {
     psg_adam_destroy(a);
     return hip_fail(e, "psg_adam_create", __FILE__, __LINE__);

@@ -56,7 +56,6 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // F_WINMISS: a cached window did not match its tile (searched inline).
 enum { F_MISSING = 0, F_WINMISS = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
 // the host-memory completion word after the flags; never zeroed by reset_flags
-constexpr int kDoneWord = F_NFLAGS;
 
 __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
   if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
@@ -1149,14 +1148,20 @@ static int run_fixup(psg_store* s, int op, const void* vals, void* out, uint64_t
   return PSG_OK;
 }
 
-// Wait for the request's kernels, then the host may read flags_host (the
-// kernels wrote it directly).  Rather than hipStreamSynchronize, the stream
-// itself writes a completion word into pinned host memory once the kernels
-// are done (hipStreamWriteValue32) and this thread spins on it: the kernels'
-// host-memory flag stores are released at kernel end, before that write.  A
-// request whose word does not appear within 2 ms (a long request, or a fault)
-// falls back to hipStreamSynchronize, which also reports any error.
-// PSG_SYNC_POLL=0 always takes hipStreamSynchronize (A/B).
+// Wait for everything enqueued on a stream so far, with its writes visible to
+// the host, to copies and to other agents, without sleeping in the runtime:
+// an event recorded behind the work, polled with hipEventQuery — the runtime's
+// own completion test, which promises what hipEventSynchronize promises — and
+// hipEventSynchronize after 2 ms (a long request, or a fault: it also reports
+// the error).  PSG_SYNC_POLL=0 always takes hipStreamSynchronize (A/B).
+//
+// Round 3 polled a word the stream wrote into pinned memory instead
+// (hipStreamWriteValue32).  Its documentation promises only that the write
+// follows the earlier commands' execution, nothing about their writes being
+// visible to the next reader, and one LR Pull reply copied to the host right
+// after that word held an earlier reply's values over a tail of the buffer
+// (GPUTEST_r03, test_lr_ref_pin[3-200000-False-True-dyadic]).  Every hand-off
+// now rests on the documented event semantics.
 static bool sync_poll() {
   static const bool on = [] {
     const char* e = getenv("PSG_SYNC_POLL");
@@ -1165,27 +1170,31 @@ static bool sync_poll() {
   return on;
 }
 
-static int read_flags(psg_store* s, hipStream_t st) {
-  if (sync_poll()) {
-    const uint32_t want = ++s->done_seq;
-    if (hipStreamWriteValue32(st, s->flags + kDoneWord, want, 0) == hipSuccess) {
-      volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(s->flags_host + kDoneWord);
-      auto t0 = std::chrono::steady_clock::now();
-      for (uint32_t spin = 0;; ++spin) {
-        if (*w == want) {
-          std::atomic_thread_fence(std::memory_order_acquire);
-          return PSG_OK;
-        }
-        if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
-        __builtin_ia32_pause();
-      }
-    } else {
-      (void)hipGetLastError();
-    }
+static int poll_event(hipEvent_t ev) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return PSG_OK;
+    if (q != hipErrorNotReady) return hip_fail(q, "hipEventQuery", __FILE__, __LINE__);
+    if ((spin & 15) == 15 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    __builtin_ia32_pause();
+  }
+  PSG_HIP(hipEventSynchronize(ev));
+  return PSG_OK;
+}
+
+static int stream_done(psg_store* s, hipStream_t st) {
+  if (sync_poll() && s->done_ev) {
+    PSG_HIP(hipEventRecord(s->done_ev, st));
+    return poll_event(s->done_ev);
   }
   PSG_HIP(hipStreamSynchronize(st));
   return PSG_OK;
 }
+
+// The request's kernels done; then the host may read flags_host (the kernels
+// wrote it directly, system-scope stores into pinned memory).
+static int read_flags(psg_store* s, hipStream_t st) { return stream_done(s, st); }
 
 template <typename T>
 static int merge_insert(psg_store* s, const uint64_t* miss, uint64_t m, hipStream_t st) {
@@ -1269,7 +1278,8 @@ static int ra_block() {
 // The window cache entry for request keys (q, n): the entry last filled for
 // them, else the least recently used one (its windows stay correct for any
 // tile whose end keys they match, so it needs no clearing).
-static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t n, uint64_t ntiles) {
+static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t n, uint64_t ntiles,
+                                      hipStream_t st) {
   psg_store::WinCache* e = nullptr;
   for (auto& c : s->wc)
     if (c.win && c.q == q && c.n == n) e = &c;
@@ -1290,7 +1300,8 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
     const uint64_t cap = std::max<uint64_t>(ntiles, 64);
     if (hipMalloc(&e->win, cap * sizeof(Win)) != hipSuccess) return nullptr;
     // gen 0 never matches a store generation: a fresh entry is all misses
-    if (hipMemset(e->win, 0, cap * sizeof(Win)) != hipSuccess) return nullptr;
+    // (stream-ordered before the request's kernels, which fill it)
+    if (hipMemsetAsync(e->win, 0, cap * sizeof(Win), st) != hipSuccess) return nullptr;
     e->cap_tiles = cap;
     e->trusted = 0;
   }
@@ -1598,7 +1609,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     }
     if (pick->cap_tiles < ntiles) PSG_TRY(drain(s));
   }
-  psg_store::WinCache* wc = win_entry(s, q, n, ntiles);
+  psg_store::WinCache* wc = win_entry(s, q, n, ntiles, st);
   PSG_REQUIRE(wc, PSG_ERR_HIP, "SORTED store: window cache allocation failed");
   Win* win = static_cast<Win*>(wc->win);
   static const int cache_on = [] {
@@ -1647,21 +1658,20 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   }
   PSG_HIP(hipGetLastError());
   // a synchronous Pull's reply is read by whoever the caller answers (a copy
-  // engine, the host, another stream): behind the kernel the stream writes the
-  // tag into a pinned word, which lands after the kernel's end-of-kernel cache
-  // write-back, so seeing it means the reply is in memory — a poll instead of
-  // a stream synchronisation (PSG_PULL_LAND=0: the synchronisation, A/B).  A
-  // request in flight skips it: the write between two kernels costs ~7 us of
-  // a back-to-back stream, so psg_store_wait synchronises once instead.
+  // engine, the host, another stream): behind the kernel an event of the ring
+  // slot is recorded, and the reply is handed out once it has completed
+  // (stream_done's semantics) — a poll instead of a stream synchronisation
+  // (PSG_PULL_LAND=0: the synchronisation, A/B).  A request in flight skips
+  // it: psg_store_wait synchronises its stream once instead.
   static const int land_on = [] {
     const char* e = getenv("PSG_PULL_LAND");
     return e ? atoi(e) : 1;
   }();
   rec->want_land = want_land && (op & PSG_PULL);
   rec->land = 0;
-  if (rec->want_land && land_on && sync_poll()) {
-    if (hipStreamWriteValue32(st, s->ring_dev + kRing + rec->ring, rec->tag, 0) == hipSuccess) rec->land = 1;
-    else (void)hipGetLastError();
+  if (rec->want_land && land_on && sync_poll() && s->land_ev[rec->ring]) {
+    PSG_HIP(hipEventRecord(s->land_ev[rec->ring], st));
+    rec->land = 1;
   }
   return PSG_OK;
 }
@@ -1703,21 +1713,12 @@ static int wait_word(psg_store* s, const InflightReq& r, uint32_t* flags) {
 static int wait_landed(psg_store* s, const InflightReq& r) {
   if (!(r.op & PSG_PULL)) return PSG_OK;
   if (!r.want_land) {  // in flight: psg_store_wait synchronises its stream
-    s->unlanded = r.stream;
+    bool known = false;
+    for (hipStream_t u : s->unlanded) known = known || u == r.stream;
+    if (!known) s->unlanded.push_back(r.stream);
     return PSG_OK;
   }
-  if (r.land) {
-    const volatile uint32_t* w = s->ring_host + kRing + r.ring;
-    auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 0;; ++spin) {
-      if (*w == r.tag) {
-        std::atomic_thread_fence(std::memory_order_acquire);
-        return PSG_OK;
-      }
-      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
-      __builtin_ia32_pause();
-    }
-  }
+  if (r.land) return poll_event(s->land_ev[r.ring]);
   PSG_HIP(hipStreamSynchronize(r.stream));
   return PSG_OK;
 }
@@ -1813,7 +1814,17 @@ static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
     int rc = wait_word(s, r, &f);
     if (rc != PSG_OK) {
       note(s, r.ticket, rc, own, own_rc);
-      s->inflight.clear();  // a lost word: the stream is broken
+      // a lost word: the stream is broken.  The arrival counters of this slot
+      // and of the requests behind it were never zeroed by a completing block
+      // — a slot used again would start from a stale count — so every set is
+      // zeroed (and the gate word cleared) once the device is idle.
+      s->inflight.clear();
+      if (hipDeviceSynchronize() == hipSuccess) {
+        constexpr size_t kCtrBytes = (size_t)kRing * (kArriveShards + 1) * kArriveStride * sizeof(uint64_t);
+        (void)hipMemset(s->done_ctr, 0, kCtrBytes);
+        (void)hipMemset(s->reject_dev + kPending, 0, sizeof(int));
+        (void)hipDeviceSynchronize();
+      }
       return rc;
     }
     if (f & W_GATED) {  // gated by a follow-up already done (or an earlier failure)
@@ -2022,18 +2033,23 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
     return rc;
   };
   hipError_t e;
-  if ((e = hipHostMalloc(&s->flags_host, (F_NFLAGS + 1) * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) !=
+  if ((e = hipHostMalloc(&s->flags_host, F_NFLAGS * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent)) !=
       hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc(flags)", __FILE__, __LINE__));
   if ((e = hipHostGetDevicePointer((void**)&s->flags, s->flags_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(flags)", __FILE__, __LINE__));
-  memset(s->flags_host, 0, (F_NFLAGS + 1) * sizeof(int));
-  if ((e = hipHostMalloc((void**)&s->ring_host, 2 * kRing * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+  memset(s->flags_host, 0, F_NFLAGS * sizeof(int));
+  if ((e = hipHostMalloc((void**)&s->ring_host, kRing * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
       hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc(completion ring)", __FILE__, __LINE__));
   if ((e = hipHostGetDevicePointer((void**)&s->ring_dev, s->ring_host, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer(completion ring)", __FILE__, __LINE__));
-  memset(s->ring_host, 0, 2 * kRing * sizeof(uint32_t));  // completion words, then landed words
+  memset(s->ring_host, 0, kRing * sizeof(uint32_t));  // completion words
+  if ((e = hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming)) != hipSuccess)
+    return fail(hip_fail(e, "hipEventCreate(completion)", __FILE__, __LINE__));
+  for (int i = 0; i < kRing; ++i)
+    if ((e = hipEventCreateWithFlags(&s->land_ev[i], hipEventDisableTiming)) != hipSuccess)
+      return fail(hip_fail(e, "hipEventCreate(landed reply)", __FILE__, __LINE__));
   if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
       (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(reject words)", __FILE__, __LINE__));
@@ -2062,6 +2078,10 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
       s->capacity = capacity;
     }
   }
+  // the memsets above ran on the null stream, which does not order with the
+  // caller's non-blocking streams: done before any request can be enqueued
+  if ((e = hipStreamSynchronize(nullptr)) != hipSuccess)
+    return fail(hip_fail(e, "hipStreamSynchronize(null stream)", __FILE__, __LINE__));
   *out = s;
   return PSG_OK;
 }
@@ -2079,6 +2099,9 @@ int psg_store_destroy(psg_store* s) {
   if (s->ring_host) (void)hipHostFree(s->ring_host);
   if (s->reject_dev) (void)hipFree(s->reject_dev);
   if (s->done_ctr) (void)hipFree(s->done_ctr);
+  if (s->done_ev) (void)hipEventDestroy(s->done_ev);
+  for (hipEvent_t ev : s->land_ev)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto& c : s->wc)
     if (c.win) (void)hipFree(c.win);
   delete s;
@@ -2163,9 +2186,11 @@ int psg_store_wait(psg_store* s, uint64_t ticket) {
   PSG_REQUIRE(s, PSG_ERR_INVALID, "psg_store_wait: null store");
   int unused = PSG_OK;
   PSG_TRY(reap(s, ticket ? ticket : ~0ull, 0, &unused));
-  if (s->unlanded) {  // reaped Pulls' replies in memory
-    hipStream_t st = s->unlanded;
-    s->unlanded = nullptr;
+  // reaped Pulls' replies in memory: every stream they ran on (a caller that
+  // switched streams drained the old one's requests into this list too)
+  while (!s->unlanded.empty()) {
+    hipStream_t st = s->unlanded.back();
+    s->unlanded.pop_back();
     PSG_HIP(hipStreamSynchronize(st));
   }
   if (s->async_rc != PSG_OK) {
@@ -2214,7 +2239,9 @@ int psg_store_slots_stretch(psg_store* s, const uint32_t* slots, uint64_t n, uin
   PSG_TRY(read_flags(s, st));
   if (s->flags_host[F_MISSING]) return PSG_OK;
   uint32_t s0 = 0;
-  PSG_HIP(hipMemcpy(&s0, slots, sizeof(s0), hipMemcpyDeviceToHost));
+  // on the caller's stream (a null-stream copy does not order with it)
+  PSG_HIP(hipMemcpyAsync(&s0, slots, sizeof(s0), hipMemcpyDeviceToHost, st));
+  PSG_HIP(hipStreamSynchronize(st));
   const uint64_t limit = s->kind == PSG_STORE_SORTED ? s->size : s->capacity;
   if (s0 != kNoSlot && (uint64_t)s0 <= limit && n <= limit - s0) *first = s0;
   return PSG_OK;

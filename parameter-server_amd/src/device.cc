@@ -94,13 +94,26 @@ std::shared_ptr<void> Alloc(size_t bytes, int dev) {
       fl.pop_back();
     }
   }
+  // PS_POOL_POISON=1 (tests): a block handed out again is first filled with
+  // 0xff bytes (NaN floats), synchronously, so a reader that overtakes the
+  // block's next writer sees NaN instead of the plausible values it held
+  static const bool poison = [] {
+    const char* e = std::getenv("PS_POOL_POISON");
+    return e && std::atoi(e) != 0;
+  }();
+  int cur = 0;
+  if (!p || poison) Check(psg_get_device(&cur), "psg_get_device");
   if (!p) {
-    int cur = 0;
-    Check(psg_get_device(&cur), "psg_get_device");
     if (cur != dev) Use(dev);
     int rc = psg_malloc(&p, rb);
     if (cur != dev) Use(cur);
     Check(rc, "psg_malloc");
+  } else if (poison) {
+    if (cur != dev) Use(dev);
+    psg_stream s = ThreadStream();
+    Check(psg_memset(p, 0xff, rb, s), "psg_memset(poison)");
+    Check(psg_stream_sync(s), "psg_stream_sync");
+    if (cur != dev) Use(cur);
   }
   return std::shared_ptr<void>(p, [dev, rb](void* q) {
     Pool& pl = GlobalPool();
@@ -176,8 +189,9 @@ void EnableAllPeerAccess() {
       if (a != b) Check(psg_enable_peer_access(a, b), "psg_enable_peer_access");
 }
 
-void CopySync(void* dst, const void* src, size_t bytes, int kind) {
-  if (!bytes) return;
+namespace {
+// One copy by the runtime on the thread stream, waited for.
+void RuntimeCopy(void* dst, const void* src, size_t bytes, int kind) {
   psg_stream s = ThreadStream();
   // a few bytes out of HBM (a hashed key list's one key): through a pinned
   // per-thread word, not a pageable destination the runtime stages itself
@@ -194,6 +208,21 @@ void CopySync(void* dst, const void* src, size_t bytes, int kind) {
   }
   Check(psg_memcpy(dst, src, bytes, kind, s), "psg_memcpy");
   Check(psg_stream_sync(s), "psg_stream_sync");
+}
+}  // namespace
+
+// Host <-> HBM copies of request and reply frames go through this runtime's
+// own pinned staging blocks (StageToDevice / StageToHost: a DMA into or out of
+// a pinned block, an event waited for, a host memcpy), not the HIP runtime's
+// pageable-memory path: what the host reads is then exactly what the DMA
+// wrote once its event completed.  (A reply copied to pageable memory by the
+// runtime's own path once held an earlier reply's bytes over a tail of the
+// buffer — GPUTEST_r03; its staging is not ours to reason about.)
+void CopySync(void* dst, const void* src, size_t bytes, int kind) {
+  if (!bytes) return;
+  if (kind == 0 && bytes > 64) return StageToDevice(dst, src, bytes);
+  if (kind == 1 && bytes > 64) return StageToHost(dst, src, bytes);
+  RuntimeCopy(dst, src, bytes, kind);
 }
 
 namespace {
@@ -249,7 +278,7 @@ void StageToDevice(void* dst_dev, const void* src_host, size_t bytes) {
   psg_stream s = ThreadStream();
   Staging* st = GetStaging();
   if (!st) {  // no pinned memory: the runtime's own pageable path
-    CopySync(dst_dev, src_host, bytes, 0);
+    RuntimeCopy(dst_dev, src_host, bytes, 0);
     return;
   }
   int b = 0;
@@ -270,7 +299,7 @@ void StageToHost(void* dst_host, const void* src_dev, size_t bytes) {
   psg_stream s = ThreadStream();
   Staging* st = GetStaging();
   if (!st) {
-    CopySync(dst_host, src_dev, bytes, 1);
+    RuntimeCopy(dst_host, src_dev, bytes, 1);
     return;
   }
   const size_t n = (bytes + kStageChunk - 1) / kStageChunk;

@@ -33,7 +33,9 @@
 #include <poll.h>
 #include <sys/mman.h>
 #include <sys/socket.h>
+#include <dirent.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -169,7 +171,10 @@ struct Ring {
     const int fd = ::shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
     if (fd < 0) return nullptr;
     const size_t bytes = kRingHdrBytes + kRingBytes;
-    if (create && ::ftruncate(fd, (off_t)bytes) != 0) {
+    // the pages reserved now (posix_fallocate): a /dev/shm too small for the
+    // ring fails here, and the connection keeps to its socket, instead of a
+    // SIGBUS in the first write that touches a page tmpfs cannot supply
+    if (create && (::ftruncate(fd, (off_t)bytes) != 0 || ::posix_fallocate(fd, 0, (off_t)bytes) != 0)) {
       ::close(fd);
       ::shm_unlink(name.c_str());
       return nullptr;
@@ -294,6 +299,24 @@ struct Ring {
     }
   }
 };
+
+// The reader's answer to a connection's ring (ReadLoop), read by the writer
+// before its first message (Connect): false — 'N', the socket closed, or no
+// answer in 10 s — leaves every byte on the socket.
+constexpr char kRingYes = 'Y', kRingNo = 'N';
+bool RingAccepted(int fd) {
+  pollfd pfd{fd, POLLIN, 0};
+  for (int waited = 0; waited < 10000; waited += 100) {
+    const int pr = ::poll(&pfd, 1, 100);
+    if (pr < 0 && errno != EINTR) return false;
+    if (pr > 0) {
+      char a = 0;
+      const ssize_t r = ::recv(fd, &a, 1, 0);
+      return r == 1 && a == kRingYes;
+    }
+  }
+  return false;
+}
 
 bool RingEnabled() {
   static const bool on = [] {
@@ -944,7 +967,9 @@ std::shared_ptr<Conn> TcpVan::Connect(int id) {
     if (!c->ring) name.clear();
   }
   const uint32_t hello[2] = {kHello, (uint32_t)name.size()};
-  if (!WriteAll(fd, hello, sizeof(hello)) || (name.size() && !WriteAll(fd, name.data(), name.size()))) return nullptr;
+  if (!WriteAll(fd, hello, sizeof(hello)) || (name.size() && !WriteAll(fd, name.data(), name.size())))
+    return nullptr;  // (c closes fd)
+  if (c->ring && !RingAccepted(fd)) c->ring.reset();  // the reader could not map it: the socket carries all
   std::lock_guard<std::mutex> lk(peers_mu_);
   auto ins = conns_.emplace(id, c);
   return ins.first->second;  // a racing connect to the same peer: keep one
@@ -1099,14 +1124,17 @@ void TcpVan::ReadLoop(int fd) {
     if (hello[1]) {
       std::string name(hello[1], '\0');
       if (!sock.read(&name[0], name.size())) return;
-      ring = Ring::Map(name, false);
-      if (!ring) {
-        // the losing side of two racing connects to one peer (Connect keeps
-        // one; the other's ring is gone with it), or a ring this process cannot
-        // map: close the connection, so a writer still using it fails loudly
-        ::shutdown(fd, SHUT_RDWR);
-        return;
-      }
+      // PS_SHM_RING_REFUSE=1 (fault injection, tests): every ring refused
+      static const bool refuse = [] {
+        const char* e = std::getenv("PS_SHM_RING_REFUSE");
+        return e && std::atoi(e) != 0;
+      }();
+      if (!refuse) ring = Ring::Map(name, false);
+      // the answer the writer waits for before its first message: 'Y' the ring
+      // carries the bytes, 'N' the socket does (a ring this process cannot map
+      // — another /dev/shm behind the same hostname, or no room in it)
+      const char ack = ring ? kRingYes : kRingNo;
+      if (!WriteAll(fd, &ack, 1)) return;
     }
   }
   struct Source {
@@ -1347,10 +1375,41 @@ static void FatalSignal(int sig) {
   ::raise(sig);
 }
 
+// A node asked where it is (SIGQUIT: the launcher's job deadline, or a person)
+// prints the stack of EVERY thread: the receiving thread signals each thread
+// of the process (/proc/self/task) with SIGUSR2, whose handler prints its own
+// backtrace under a spin lock, one thread at a time; then the process goes on.
+static std::atomic<int> g_dump_lock{0};
+static void DumpOwnStack(int) {
+  while (g_dump_lock.exchange(1, std::memory_order_acquire)) {
+  }
+  char msg[96];
+  const int n = std::snprintf(msg, sizeof(msg), "[node %d] thread %d:\n", (int)getpid(), (int)gettid());
+  if (n > 0) (void)!::write(2, msg, (size_t)n);
+  void* frames[48];
+  const int k = ::backtrace(frames, 48);
+  ::backtrace_symbols_fd(frames, k, 2);
+  g_dump_lock.store(0, std::memory_order_release);
+}
+static void DumpAllStacks(int) {
+  char msg[80];
+  const int n = std::snprintf(msg, sizeof(msg), "[node %d] SIGQUIT: stacks of every thread follow\n", (int)getpid());
+  if (n > 0) (void)!::write(2, msg, (size_t)n);
+  if (DIR* d = ::opendir("/proc/self/task")) {
+    while (dirent* e = ::readdir(d)) {
+      const int tid = std::atoi(e->d_name);
+      if (tid > 0) ::syscall(SYS_tgkill, (int)getpid(), tid, SIGUSR2);
+    }
+    ::closedir(d);
+  }
+}
+
 int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** argv) {
   const char* role = RoleOf(argc, argv);
   CHECK(role) << "process mode needs a role (argv[3] or PS_ROLE)";
   for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL}) ::signal(sig, FatalSignal);
+  ::signal(SIGUSR2, DumpOwnStack);
+  ::signal(SIGQUIT, DumpAllStacks);
   ReadLocalConfigToEnv(argv[1]);
   shm::Enable();
   const int ns = Environment::GetIntOrDefault("PS_NUM_SERVER", 1);
@@ -1455,11 +1514,28 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
   spawn("scheduler", 0);
   for (int i = 0; i < num_servers; ++i) spawn("server", i);
   for (int i = 0; i < num_workers; ++i) spawn("worker", i);
-  // wait; once a node failed, give the others (which get the ABORT) 30 s
+  // wait; once a node failed, give the others (which get the ABORT) 30 s.
+  // PS_JOB_TIMEOUT_S: a job still running then is hung — every node prints
+  // the stacks of all its threads (SIGQUIT, DumpAllStacks), then all are killed
   int rc = 0;
   size_t left = pids.size();
   auto failed_at = std::chrono::steady_clock::time_point::max();
+  const int job_timeout_s = Environment::GetIntOrDefault("PS_JOB_TIMEOUT_S", 0);
+  auto job_deadline = job_timeout_s > 0 ? std::chrono::steady_clock::now() + std::chrono::seconds(job_timeout_s)
+                                              : std::chrono::steady_clock::time_point::max();
   while (left) {
+    if (std::chrono::steady_clock::now() > job_deadline) {
+      std::fprintf(stderr, "[launcher] job still running after PS_JOB_TIMEOUT_S=%d s: stacks of every node follow\n",
+                   job_timeout_s);
+      for (pid_t q : pids) {  // one node at a time: their dumps share stderr
+        kill(q, SIGQUIT);
+        std::this_thread::sleep_for(std::chrono::milliseconds(500));
+      }
+      for (pid_t q : pids) kill(q, SIGKILL);
+      rc = 124;
+      failed_at = std::chrono::steady_clock::time_point::max();
+      job_deadline = std::chrono::steady_clock::time_point::max();
+    }
     int status = 0;
     pid_t p = waitpid(-1, &status, WNOHANG);
     if (p > 0) {

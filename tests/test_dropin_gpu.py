@@ -23,7 +23,9 @@ BIN = os.path.join(ROOT, "tests", "_bin")
 
 
 def run(path, *args, timeout=300, env=None):
-    e = dict(os.environ, **(env or {}))
+    # recycled HBM blocks start as NaN (device::Alloc): a reply read before
+    # its kernel wrote it fails the harness's known-answer CHECKs
+    e = dict(os.environ, PS_POOL_POISON="1", **(env or {}))
     return subprocess.run([path, *map(str, args)], capture_output=True, text=True, timeout=timeout,
                           env=e)
 

@@ -472,6 +472,35 @@ def test_async_requests_with_absent_keys_replay_in_order(depth):
     np.testing.assert_array_equal(gv, ov)
 
 
+def test_async_pull_replies_on_two_streams_are_in_memory_after_wait():
+    """psg_store_wait promises every reaped Pull's reply is in memory.  Pulls
+    in flight on stream A, then on stream B (the switch reaps A's requests),
+    then wait(): each reply is read by a copy on a THIRD stream, ordered with
+    neither, with no device synchronisation in between."""
+    rng = np.random.default_rng(5)
+    k = np.unique(rng.integers(0, KMAX, 300000, dtype=np.uint64))
+    n = len(k)
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    dk = dev(k)
+    sa, sb, sc = psg.Stream(), psg.Stream(), psg.Stream()
+    outs, exps = [], []
+    for rep in range(8):
+        v = rng.uniform(-1, 1, n).astype(np.float32)
+        st.handle(psg.PUSH, dk, dev(v), None, n, stream=sa)
+        orc.handle(oracle.PUSH, k, v, n)
+        for s in (sa, sa, sb, sb):
+            out = psg.DeviceBuffer(n * 4)
+            st.handle_async(psg.PULL, dk, None, out, n, stream=s)
+            outs.append(out)
+            exps.append(orc.handle(oracle.PULL, k, None, n))
+        st.wait()
+        for out, exp in zip(outs, exps):
+            np.testing.assert_array_equal(out.download(np.float32, n, stream=sc), exp)
+        outs.clear()
+        exps.clear()
+
+
 def test_async_request_failure_is_reported_by_wait():
     st = psg.Store(psg.SORTED, psg.F32, 0, 1 << 40, 0)
     k = np.arange(1000, dtype=np.uint64) * 7

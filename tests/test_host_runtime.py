@@ -17,10 +17,18 @@ DROPIN = os.path.join(ROOT, "tests", "_dropin")
 
 def run(path, *args, timeout=120, env=None):
     e = dict(os.environ)
+    if "-procs" in map(str, args):
+        # a process job still running 15 s before the test's limit is hung: the
+        # launcher has every node print the stacks of all its threads (SIGQUIT)
+        # and kills the job, so the failure says where it stopped
+        e["PS_JOB_TIMEOUT_S"] = str(max(5, timeout - 15))
     if env:
         e.update(env)
-    return subprocess.run([path, *map(str, args)], capture_output=True, text=True, timeout=timeout,
-                          env=e)
+    r = subprocess.run([path, *map(str, args)], capture_output=True, text=True, timeout=timeout, env=e)
+    if r.returncode == 124 and "PS_JOB_TIMEOUT_S" in r.stderr:
+        # the whole dump, not a tail: which node waits where is the evidence
+        print(r.stderr)
+    return r
 
 
 def _need(path):
@@ -247,3 +255,14 @@ def test_process_mode_message_ring(ring):
     assert line["iters"] == 5000 and line["us_per_request"] > 0
     print(line)
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("psgring.")]
+
+
+def test_process_mode_refused_ring_falls_back_to_the_socket():
+    """A reader that cannot map a connection's shared-memory ring (another
+    /dev/shm behind the same hostname, or no room in it) answers 'N' and the
+    writer keeps every byte on the socket: the job still completes."""
+    exe = os.path.join(BIN, "kv_cluster_host")
+    _need(exe)
+    r = run(exe, "-ns", 2, "-nw", 2, "-procs", 300000, env={"PS_SHM_RING_REFUSE": "1"}, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count(" ok") == 2
