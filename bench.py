@@ -110,6 +110,24 @@ class GpuBackend:
             self.begins, self.ends = p.server_ranges(self.world)
             self.store = p.Store(p.SORTED, self.dt, int(self.begins[self.rank]),
                                  int(self.ends[self.rank]), 0)
+            extra = int(os.environ.get("PSG_BENCH_STORE_EXTRA", "0"))
+            if extra > 0 and self.world == 1:
+                # a store that holds `extra` more keys per request key, between
+                # them (the request is then every (extra+1)-th key of the store,
+                # not a stretch of it: the general fused path, not the identity
+                # one); inserted once with value 0 by a Pull, as operator[] does
+                kk = k.astype(np.uint64)
+                gaps = np.diff(kk)
+                assert np.all(gaps > extra), "keys too dense for the extra store keys"
+                more = [kk[:-1] + (gaps // (extra + 1)) * np.uint64(j) for j in range(1, extra + 1)]
+                sk = np.unique(np.concatenate([kk] + more))
+                dsk = p.DeviceBuffer.from_numpy(sk)
+                tmp = p.DeviceBuffer(len(sk) * self.vb)
+                self.store.handle(p.PULL, dsk, None, tmp, len(sk), stream=self.stream)
+                self.sync()
+                tmp.free()
+                dsk.free()
+                self.store_extra = extra
         else:
             self.store = p.Store(p.DENSE, self.dt, lo, lo + blk, blk)
         self.vals = p.DeviceBuffer(L * self.vb)
@@ -655,20 +673,35 @@ class GpuBackend:
         b2b_ms = statistics.median(eb[i].elapsed_ms(eb[i + 1]) for i in range(iters))
         bad, _ = p.verify_synth_sum(o, n, p.F32, self._seed, 1, 0.0, 1000.0, float(warm + iters),
                                     stream=self.stream)  # the last Pull, before the b2b Pushes
-        # this box's own copy ceiling: the runtime's device-to-device copy of
-        # the same 1 GiB (read + write), so a kernel's fraction can be read
-        # against what this GPU's HBM and page placement give a plain copy
-        # (MI355X_MICROARCH.md quotes 6.29 TB/s from one box; boxes differ)
+        # this process's own copy ceiling on the same two buffers: the Pull's
+        # traffic is exactly a copy's (read 1 GiB, write 1 GiB), so the best of
+        # a few shapes of the plain float4 streaming copy kernel (psg_copy:
+        # vectors per lane in flight x blocks per CU) is what this GPU and this
+        # process's page placement give the Pull (MI355X_MICROARCH.md quotes
+        # 6.29 TB/s from one box; processes on one box differ by up to 10 %)
         self.sync()
-        ec = [p.Event() for _ in range(11)]
+        copy_shapes = {}
+        for unroll, bpc in ((1, 4), (2, 2), (4, 2), (4, 3), (8, 2)):
+            for _ in range(2):
+                p.copy(o, v, n * 4, unroll, bpc, stream=self.stream)
+            ec = [p.Event() for _ in range(11)]
+            ec[0].record(self.stream)
+            for i in range(10):
+                p.copy(o, v, n * 4, unroll, bpc, stream=self.stream)
+                ec[i + 1].record(self.stream)
+            self.sync()
+            copy_shapes[f"U{unroll}x{bpc}/CU"] = statistics.median(ec[i].elapsed_ms(ec[i + 1]) for i in range(10))
+        best_shape = min(copy_shapes, key=copy_shapes.get)
+        copy_ms = copy_shapes[best_shape]
+        em = [p.Event() for _ in range(11)]
         for _ in range(2):
             p.memcpy_d2d(o, v, n * 4, stream=self.stream)
-        ec[0].record(self.stream)
+        em[0].record(self.stream)
         for i in range(10):
             p.memcpy_d2d(o, v, n * 4, stream=self.stream)
-            ec[i + 1].record(self.stream)
+            em[i + 1].record(self.stream)
         self.sync()
-        copy_ms = statistics.median(ec[i].elapsed_ms(ec[i + 1]) for i in range(10))
+        memcpy_ms = statistics.median(em[i].elapsed_ms(em[i + 1]) for i in range(10))
         st.close()
         v.free()
         o.free()
@@ -680,11 +713,14 @@ class GpuBackend:
             out[f"{name}_frac"] = round(gbs / HBM_PEAK_GBS, 4)
         out["push_back_to_back_frac"] = round(PUSH_ACCESSES * 4 * n / (b2b_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         copy_gbs = 2 * 4 * n / (copy_ms * 1e-3) / 1e9
-        out["copy_ceiling"] = {"what": "hipMemcpyAsync device-to-device of the same 1 GiB, read + write bytes",
-                               "ms": round(copy_ms, 5), "achieved": round(copy_gbs, 1),
+        out["copy_ceiling"] = {"what": "psg_copy float4 streaming copy of the same 1 GiB (read + write bytes), "
+                                       "best median of 5 shapes, same process and buffers",
+                               "best_shape": best_shape, "ms": round(copy_ms, 5), "achieved": round(copy_gbs, 1),
                                "frac": round(copy_gbs / HBM_PEAK_GBS, 4),
+                               "shapes_ms": {k: round(x, 5) for k, x in copy_shapes.items()},
                                "push_of_copy": round(out["push_achieved"] / copy_gbs, 4),
-                               "pull_of_copy": round(out["pull_achieved"] / copy_gbs, 4)}
+                               "pull_of_copy": round(out["pull_achieved"] / copy_gbs, 4),
+                               "hipmemcpy_d2d_achieved": round(2 * 4 * n / (memcpy_ms * 1e-3) / 1e9, 1)}
         out["kernel"] = "k_dense_vec<PUSH> / <PULL>, 12 / 8 B per float"
         return out
 
@@ -870,6 +906,9 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         # the identity pair once the key list's windows are trusted
         paths = backend.store.counters()
         res["keyed_paths"] = paths
+        if getattr(backend, "store_extra", 0):
+            res["config"]["store_keys"] = (f"{backend.store_extra + 1} x the request's: the request is every "
+                                           f"{backend.store_extra + 1}-th store key (PSG_BENCH_STORE_EXTRA)")
         if paths["ident"] > 0 and paths["notident"] == 0:
             kname = ("SORTED-store Push: k_ident_check + k_ident_apply (identity request: the key "
                      "list is the stretch K[D, D + n) of the store's keys, D from its first tile's "

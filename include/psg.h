@@ -106,6 +106,13 @@ int psg_host_unregister(void* hptr);
 /* kind: 0 = H2D, 1 = D2H, 2 = D2D, 3 = default (unified addressing) */
 int psg_memcpy(void* dst, const void* src, size_t bytes, int kind, psg_stream stream);
 int psg_memset(void* dptr, int value, size_t bytes, psg_stream stream);
+/* A plain 16-B-per-lane streaming copy (non-temporal loads and stores, grid
+ * stride) of `bytes` (a multiple of 16, both pointers 16-B aligned), with
+ * `unroll` vectors per lane in flight (1, 2, 4 or 8) at `blocks_per_cu`
+ * 256-thread blocks per CU (1..16): the HBM copy ceiling a Pull — whose traffic
+ * is exactly a copy's, read the store, write the reply — is measured against in
+ * the same process (bench.py).  Not on any request path. */
+int psg_copy(void* dst, const void* src, uint64_t bytes, int unroll, int blocks_per_cu, psg_stream stream);
 
 int psg_stream_create(psg_stream* stream);
 int psg_stream_destroy(psg_stream stream);

@@ -430,3 +430,21 @@ int slot_request(int dtype, int op, void* store_vals, const uint32_t* slots, con
 }
 
 }  // namespace psg
+
+extern "C" int psg_copy(void* dst, const void* src, uint64_t bytes, int unroll, int blocks_per_cu,
+                        psg_stream stream) {
+  using namespace psg;
+  if (bytes == 0) return PSG_OK;
+  PSG_REQUIRE(dst && src && aligned16(dst) && aligned16(src) && bytes % 16 == 0, PSG_ERR_INVALID,
+              "psg_copy: 16-B aligned pointers and a multiple of 16 bytes");
+  PSG_REQUIRE((unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) && blocks_per_cu >= 1 && blocks_per_cu <= 16,
+              PSG_ERR_INVALID, "psg_copy: unroll 1/2/4/8, 1..16 blocks per CU");
+  DenseCfg c;
+  c.unroll = unroll;
+  c.nt = 3;  // non-temporal loads (the "store" operand is the source) and stores
+  c.blocks_per_cu = blocks_per_cu;
+  // a Pull with the source as its store: load 16 B, store 16 B, nothing else
+  dispatch_vec<PSG_F32, PSG_PULL>(c, const_cast<void*>(src), nullptr, dst, bytes / 16, (hipStream_t)stream);
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}

@@ -218,6 +218,8 @@ struct psg_store {
     int trusted;         // skip the search pre-pass; the kernel still verifies
     int strikes;         // kernel-detected stale windows for this (q, n)
     uint32_t ident_fail; // K's generation at which an identity request on this list was not one
+    uint32_t ident_ok;   // K's generation at which an identity request on this list completed as one
+    uint64_t ident_trial;  // ticket of the identity attempt in flight before either is known (0: none)
   } wc[4];
   uint64_t wc_clock;
   uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters

@@ -625,32 +625,88 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
     uint32_t r = 0;
     uint64_t slot[kPerLane];
     bool hit[kPerLane];
+    if (staged) {
 #pragma unroll
-    for (int k = 0; k < kPerLane; ++k) {
-      const uint64_t i = i0 + k;
-      hit[k] = false;
-      slot[k] = 0;
-      if (i >= t1) continue;
-      const uint64_t kk = key[k];
-      uint64_t p;
-      bool found;
-      if (staged) {
+      for (int k = 0; k < kPerLane; ++k) {
+        const uint64_t i = i0 + k;
+        hit[k] = false;
+        slot[k] = 0;
+        if (i >= t1) continue;
+        const uint64_t kk = key[k];
         const uint32_t w = (uint32_t)W;
         if (k == 0) {
           r = lower_bound_lds(sK, w, kk);
         } else if (!(r < w && sK[r] >= kk)) {
-          if (r + 1 < w && sK[r + 1] >= kk) r = r + 1;
-          else r = (r + 1 >= w) ? w : r + 1 + lower_bound_lds(sK + r + 1, w - r - 1, kk);
+          // gallop forward from the previous key's place (probes at +1, +2,
+          // +4, ... then a search of the last gap): the next store key for a
+          // request that covers its stretch of the store, two or three probes
+          // for one that asks for every other or every third key — where a
+          // search of the whole rest of the window took ~13 dependent LDS reads
+          // (r == w: the previous key is past the window, and so is this one)
+          uint32_t a = r < w ? r + 1 : w, b = a, step = 1;  // sK[a - 1] < kk
+          while (b < w && sK[b] < kk) {
+            a = b + 1;
+            b = a + step;
+            step <<= 1;
+          }
+          if (b > w) b = w;
+          if (a > b) a = b;  // (a <= w always; kept explicit: b - a is a count)
+          r = a + lower_bound_lds(sK + a, b - a, kk);
         }
-        p = lo + r;
-        found = r < w && sK[r] == kk;
-      } else {
-        p = lower_bound_dev(K, lo, hi, kk);
-        found = p < S && K[p] == kk;
+        const bool found = r < w && sK[r] == kk;
+        hit[k] = found;
+        slot[k] = lo + r;
+        if (!found) missing++;
       }
-      hit[k] = found;
-      slot[k] = p;
-      if (!found) missing++;
+    } else if (W <= 16 * (uint64_t)winN) {
+      // The window is larger than the LDS holds: a request sparse in the store
+      // (the store holds more keys than the tile asks for — every other key,
+      // say).  Both the tile's keys and the window ascend, so the window
+      // streams through LDS in winN-key chunks and chunk c places exactly the
+      // keys between its first and last store key: the window is read once,
+      // where a search per key in HBM made dependent round trips per key
+      // (2.4x the kernel time at every other key).  Block-uniform loop.
+      bool open[kPerLane];
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        hit[k] = false;
+        slot[k] = 0;
+        open[k] = i0 + k < t1;
+      }
+      for (uint64_t c0 = lo; c0 < hi; c0 += winN) {
+        const uint32_t wc = (uint32_t)(hi - c0 < (uint64_t)winN ? hi - c0 : (uint64_t)winN);
+        __syncthreads();  // the previous chunk's readers are done with sK
+        stage_window<NT>(sK, K, c0, wc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint64_t clast = sK[wc - 1];
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) {
+          if (open[k] && key[k] <= clast) {
+            const uint32_t rc = lower_bound_lds(sK, wc, key[k]);
+            hit[k] = sK[rc] == key[k];
+            slot[k] = c0 + rc;
+            open[k] = false;
+          }
+        }
+        if (clast >= qlast) break;  // every key of the tile placed (uniform)
+      }
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k)
+        if (i0 + k < t1 && !hit[k]) missing++;  // (keys past the window's end: absent)
+    } else {
+      // sparser still (under one key in 32 of the window): a search per key
+      // in HBM reads less than the window would
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        hit[k] = false;
+        slot[k] = 0;
+        if (i0 + k >= t1) continue;
+        const uint64_t p = lower_bound_dev(K, lo, hi, key[k]);
+        hit[k] = p < S && K[p] == key[k];
+        slot[k] = p;
+        if (!hit[k]) missing++;
+      }
     }
     if (tile + gridDim.x >= ntiles) {  // this block's last tile (uniform)
       after = block_arrive((missing ? 1u : 0u) | (winmiss ? 2u : 0u) | (range ? 4u : 0u) | (unsorted ? 8u : 0u),
@@ -1292,6 +1348,8 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
     e->trusted = 0;
     e->strikes = 0;
     e->ident_fail = 0;
+    e->ident_ok = 0;
+    e->ident_trial = 0;
   }
   if (e->cap_tiles < ntiles) {
     if (e->win) (void)hipFree(e->win);
@@ -1619,7 +1677,14 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   const bool trusted = cache_on && wc->trusted != 0 && (uint32_t)wc->trusted == s->gen;
   // trusted windows of a key list whose identity attempt has not failed
   // against this K: the identity kernels (no validation pass, no search)
-  const bool ident = trusted && ident_on() && wc->ident_fail != s->gen;
+  // ... and one speculative attempt at a time: until an identity request on
+  // this list has completed as one against this K, the requests launched
+  // behind an attempt in flight take the general path (a list that is not a
+  // stretch would otherwise have every request in flight attempted, rejected
+  // and replayed before the first verdict is reaped)
+  bool ident = trusted && ident_on() && wc->ident_fail != s->gen;
+  const bool trial = ident && wc->ident_ok != s->gen;
+  if (trial && wc->ident_trial != 0) ident = false;
   const int seq = next_seq(s);
   // search blocks: one wave per window bound (2 per tile); key-stream blocks:
   // 2048 keys each, capped at the streaming grid.  A Pull checks its keys
@@ -1631,6 +1696,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
                                                          s->key_begin, s->key_end, s->reject_dev, seq,
                                                          aligned16(q) ? 1 : 0);
   rec->ticket = ++s->next_ticket;
+  if (ident && trial) wc->ident_trial = rec->ticket;
   rec->op = op;
   rec->q = q;
   rec->n = n;
@@ -1731,9 +1797,19 @@ static int wait_landed(psg_store* s, const InflightReq& r) {
 template <int DT>
 static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc);
 
+// An identity request's verdict for its key list: a completed one proves the
+// list a stretch of this K; either way the attempt is no longer in flight.
+static void end_ident(psg_store* s, const InflightReq& r, bool completed_as_one) {
+  psg_store::WinCache& wc = s->wc[r.wc];
+  if (!r.ident || wc.q != r.q || wc.n != r.n) return;
+  if (wc.ident_trial == r.ticket) wc.ident_trial = 0;
+  if (completed_as_one) wc.ident_ok = s->gen;
+}
+
 template <int DT>
 static int finish(psg_store* s, const InflightReq& r, uint32_t f) {
   psg_store::WinCache& wc = s->wc[r.wc];
+  end_ident(s, r, !(f & (W_NOTIDENT | W_RANGE)));
   if (f & W_NOTIDENT) {
     // not an identity request after all: it wrote nothing to the store (a
     // Pull, only its reply).  No identity attempt on this key list until K
@@ -1797,6 +1873,7 @@ static void note(psg_store* s, uint64_t ticket, int rc, uint64_t own, int* own_r
 template <int DT>
 static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
   auto replay = [&](const InflightReq& g) {
+    end_ident(s, g, false);  // gated: no verdict
     InflightReq r2;
     int rc = launch_fused<DT>(s, g.op, g.q, g.n, g.vals, g.out, g.stream, &r2, g.want_land != 0);
     if (rc == PSG_OK) {
@@ -1819,6 +1896,7 @@ static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
       // — a slot used again would start from a stale count — so every set is
       // zeroed (and the gate word cleared) once the device is idle.
       s->inflight.clear();
+      for (auto& c : s->wc) c.ident_trial = 0;
       if (hipDeviceSynchronize() == hipSuccess) {
         constexpr size_t kCtrBytes = (size_t)kRing * (kArriveShards + 1) * kArriveStride * sizeof(uint64_t);
         (void)hipMemset(s->done_ctr, 0, kCtrBytes);
@@ -1844,6 +1922,7 @@ static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
       if (rc != PSG_OK) {
         note(s, g.ticket, rc, own, own_rc);
         s->inflight.clear();
+        for (auto& c : s->wc) c.ident_trial = 0;
         return rc;
       }
       later.emplace_back(g, gf);
@@ -2179,6 +2258,13 @@ int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys, uint64
   PSG_TRY(launch_fused_any(s, flags, keys, n, vals, out, st, &rec, false));
   s->inflight.push_back(rec);
   *ticket = rec.ticket;
+  // an identity trial is reaped before anything is launched behind it: if the
+  // list is not a stretch it raises kPending, and every request launched
+  // behind it would be gated and launched again
+  if (rec.ident && s->wc[rec.wc].ident_trial == rec.ticket) {
+    int unused = PSG_OK;
+    PSG_TRY(reap(s, rec.ticket, 0, &unused));
+  }
   return PSG_OK;
 }
 

@@ -36,7 +36,7 @@ EXPORTS = [
     "psg_abi_version", "psg_last_error", "psg_device_count", "psg_set_device",
     "psg_get_device", "psg_device_sync", "psg_enable_peer_access", "psg_malloc", "psg_free", "psg_host_alloc",
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
-    "psg_memset", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
+    "psg_memset", "psg_copy", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
     "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
     "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",
@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
             "psg_host_register": ([vp, C.c_size_t], i32), "psg_host_unregister": ([vp], i32),
             "psg_memcpy": ([vp, vp, C.c_size_t, i32, vp], i32),
             "psg_memset": ([vp, i32, C.c_size_t, vp], i32),
+            "psg_copy": ([vp, vp, u64, i32, i32, vp], i32),
             "psg_stream_create": ([C.POINTER(vp)], i32), "psg_stream_destroy": ([vp], i32),
             "psg_stream_sync": ([vp], i32), "psg_event_create": ([C.POINTER(vp)], i32),
             "psg_event_destroy": ([vp], i32), "psg_event_record": ([vp, vp], i32),
@@ -299,6 +300,11 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def copy(dst, src, nbytes: int, unroll: int = 1, blocks_per_cu: int = 4, stream=None) -> None:
+    """psg_copy: the streaming float4 copy kernel (the Pull's copy ceiling)."""
+    _call("psg_copy", C.c_void_p(_ptr(dst)), C.c_void_p(_ptr(src)), nbytes, unroll, blocks_per_cu, _s(stream))
 
 
 def memcpy_d2d(dst, src, nbytes: int, stream=None) -> None:

@@ -579,6 +579,49 @@ def test_sorted_window_cache_transitions(dtype):
     np.testing.assert_array_equal(gv.view(NPT[dtype]), ov)
 
 
+@pytest.mark.parametrize("every", [2, 3, 5, 40])
+def test_sorted_requests_sparse_in_the_store(every):
+    """A request that asks for every `every`-th key of a larger store: its
+    tiles' windows of store keys exceed the LDS window (k_resolve_apply then
+    streams each window through LDS in chunks; past 16 chunks, every 40th key,
+    it searches each key in HBM).  Push, PushPull and Pull in flight and
+    synchronous, against the oracle, then the whole store."""
+    rng = np.random.default_rng(1000 + every)
+    univ = np.unique(rng.integers(1 << 20, 1 << 62, 600000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    v0 = rng.uniform(-1, 1, len(univ)).astype(np.float32)
+    st.handle(psg.PUSH, dev(univ), dev(v0), None, len(univ))
+    orc.handle(oracle.PUSH, univ, v0, len(univ))
+    k = univ[1::every].copy()
+    n = len(k)
+    dk = dev(k)
+    outs = []
+    for j in range(12):
+        flags = [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL][j % 3]
+        v = rng.uniform(-1, 1, n).astype(np.float32)
+        out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+        if j < 6:
+            st.handle(flags, dk, dev(v) if flags & psg.PUSH else None, out, n)
+        else:
+            st.handle_async(flags, dk, dev(v) if flags & psg.PUSH else None, out, n)
+        exp = orc.handle(flags, k, v if flags & psg.PUSH else None, n)
+        if out is not None:
+            outs.append((out, exp, j))
+    st.wait()
+    psg.device_sync()
+    for out, exp, j in outs:
+        np.testing.assert_array_equal(out.download(np.float32, n), exp, err_msg=f"request {j}")
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv, ov)
+    # the list is not a stretch of the store: at most one identity attempt
+    # (rejected), never one per request in flight
+    c = st.counters()
+    assert c["ident"] <= 1 and c["notident"] <= 1, c
+
+
 def test_dense_keyed_out_of_range_rejected_out_of_order_applied():
     st = psg.Store(psg.DENSE, psg.F32, 100, 100000, 5000)
     base = np.arange(5000, dtype=np.float32)
