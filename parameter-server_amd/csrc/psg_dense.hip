@@ -35,11 +35,13 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
 }
 
 // Vector kernel over nvec 16-byte vectors.  OP bits: PSG_PUSH, PSG_PULL.
-template <int DT, int OP, int U, int NT>
-__global__ __launch_bounds__(256) void k_dense_vec(u32x4* __restrict__ store,
-                                                   const u32x4* __restrict__ vals,
-                                                   u32x4* __restrict__ out, uint64_t nvec) {
+// BS threads per block (256, or 512 / 1024 for the shapes dense_cfg picks).
+template <int DT, int OP, int U, int NT, int BS = 256>
+__global__ __launch_bounds__(BS) void k_dense_vec(u32x4* __restrict__ store,
+                                                  const u32x4* __restrict__ vals,
+                                                  u32x4* __restrict__ out, uint64_t nvec) {
   using E = Elem<DT>;
+  constexpr int kBlock = BS;
   const uint64_t tile = (uint64_t)kBlock * U;
   const uint64_t gstride = (uint64_t)gridDim.x * tile;
   for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec; base += gstride) {
@@ -201,6 +203,7 @@ struct DenseCfg {
   int unroll = 2;
   int nt = -1;  // -1: by store size
   int blocks_per_cu = 2;
+  int block = 256;  // threads per block: 256, 512 or 1024 (PSG_DENSE_BLOCK)
 };
 static DenseCfg dense_cfg() {
   static DenseCfg cfg = [] {
@@ -208,6 +211,8 @@ static DenseCfg dense_cfg() {
     if (const char* e = getenv("PSG_DENSE_UNROLL")) c.unroll = atoi(e);
     if (const char* e = getenv("PSG_DENSE_NT")) c.nt = atoi(e);
     if (const char* e = getenv("PSG_DENSE_BPC")) c.blocks_per_cu = atoi(e);
+    if (const char* e = getenv("PSG_DENSE_BLOCK")) c.block = atoi(e);
+    if (c.block != 256 && c.block != 512 && c.block != 1024) c.block = 256;
     if (c.unroll != 1 && c.unroll != 2 && c.unroll != 4 && c.unroll != 8) c.unroll = 2;
     if (c.blocks_per_cu < 1 || c.blocks_per_cu > 32) c.blocks_per_cu = 2;
     if (c.nt < -1 || c.nt > 3) c.nt = -1;
@@ -288,25 +293,39 @@ static unsigned stream_grid(uint64_t units, uint64_t per_block, int bpc) {
   return (unsigned)b;
 }
 
-template <int DT, int OP, int U, int NT>
+template <int DT, int OP, int U, int NT, int BS = 256>
 static void launch_vec(void* store, const void* vals, void* out, uint64_t nvec, int bpc,
                        hipStream_t s) {
-  unsigned g = stream_grid(nvec, (uint64_t)kBlock * U, bpc);
-  k_dense_vec<DT, OP, U, NT><<<g, kBlock, 0, s>>>((u32x4*)store, (const u32x4*)vals, (u32x4*)out,
-                                                  nvec);
+  unsigned g = stream_grid(nvec, (uint64_t)BS * U, bpc);
+  k_dense_vec<DT, OP, U, NT, BS><<<g, BS, 0, s>>>((u32x4*)store, (const u32x4*)vals, (u32x4*)out, nvec);
 }
 
 template <int DT, int OP>
 static void dispatch_vec(const DenseCfg& c, void* store, const void* vals, void* out,
                          uint64_t nvec, hipStream_t s) {
-#define PSG_V(U, NT)                                                      \
-  if (c.unroll == U && c.nt == NT) {                                      \
-    launch_vec<DT, OP, U, NT>(store, vals, out, nvec, c.blocks_per_cu, s); \
-    return;                                                               \
+#define PSG_V(U, NT)                                                                \
+  if (c.unroll == U && c.nt == NT && c.block == 256) {                              \
+    launch_vec<DT, OP, U, NT>(store, vals, out, nvec, c.blocks_per_cu, s);           \
+    return;                                                                         \
+  }
+#define PSG_VB(U, NT, BS)                                                           \
+  if (c.unroll == U && c.nt == NT && c.block == BS) {                               \
+    launch_vec<DT, OP, U, NT, BS>(store, vals, out, nvec, c.blocks_per_cu, s);       \
+    return;                                                                         \
   }
   PSG_V(1, 0) PSG_V(1, 1) PSG_V(1, 2) PSG_V(1, 3) PSG_V(2, 0) PSG_V(2, 1) PSG_V(2, 2) PSG_V(2, 3)
   PSG_V(4, 0) PSG_V(4, 1) PSG_V(4, 2) PSG_V(4, 3) PSG_V(8, 0) PSG_V(8, 1) PSG_V(8, 2) PSG_V(8, 3)
+  PSG_VB(1, 1, 512) PSG_VB(1, 3, 512) PSG_VB(2, 1, 512) PSG_VB(2, 3, 512)
+  PSG_VB(1, 1, 1024) PSG_VB(1, 3, 1024) PSG_VB(2, 1, 1024) PSG_VB(2, 3, 1024)
+#undef PSG_VB
 #undef PSG_V
+  // a shape without an instantiation: the same threads per CU in 256-thread
+  // blocks (unroll and nt are validated by dense_cfg: the 256 table has them all)
+  if (c.block == 256) return;
+  DenseCfg d = c;
+  d.block = 256;
+  d.blocks_per_cu = c.blocks_per_cu * c.block / 256;
+  dispatch_vec<DT, OP>(d, store, vals, out, nvec, s);
 }
 
 template <int DT, int OP>

@@ -119,17 +119,19 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   std::vector<Shape> shapes = {
-      {"U1 B256 8/CU (library)", go<1, 256, true, false>, go<1, 256, false, false>, 8},
-      {"U1 B256 6/CU", go<1, 256, true, false>, go<1, 256, false, false>, 6},
+      {"U1 B256 8/CU", go<1, 256, true, false>, go<1, 256, false, false>, 8},
+      {"U2 B256 2/CU", go<2, 256, true, false>, go<2, 256, false, false>, 2},
+      {"U1 B256 4/CU", go<1, 256, true, false>, go<1, 256, false, false>, 4},
+      {"U1 B512 2/CU", go<1, 512, true, false>, go<1, 512, false, false>, 2},
       {"U1 B512 4/CU", go<1, 512, true, false>, go<1, 512, false, false>, 4},
+      {"U1 B512 3/CU", go<1, 512, true, false>, go<1, 512, false, false>, 3},
       {"U1 B1024 2/CU", go<1, 1024, true, false>, go<1, 1024, false, false>, 2},
-      {"U2 B256 4/CU", go<2, 256, true, false>, go<2, 256, false, false>, 4},
+      {"U1 B1024 1/CU", go<1, 1024, true, false>, go<1, 1024, false, false>, 1},
       {"U2 B512 2/CU", go<2, 512, true, false>, go<2, 512, false, false>, 2},
-      {"U4 B256 2/CU", go<4, 256, true, false>, go<4, 256, false, false>, 2},
-      {"U1 B256 16/CU", go<1, 256, true, false>, go<1, 256, false, false>, 16},
-      {"chunk U1 B256 8/CU", go<1, 256, true, true>, go<1, 256, false, true>, 8},
-      {"chunk U2 B512 2/CU", go<2, 512, true, true>, go<2, 512, false, true>, 2},
+      {"U2 B256 4/CU", go<2, 256, true, false>, go<2, 256, false, false>, 4},
+      {"U2 B1024 1/CU", go<2, 1024, true, false>, go<2, 1024, false, false>, 1},
   };
+
   const int steps = 30;
   std::vector<hipEvent_t> ev(2 * steps + 1);
   for (auto& e : ev) CK(hipEventCreate(&e));
