@@ -257,11 +257,18 @@ static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op) {
     // 2,454-2,517 GB/s against 2,419-2,435 at 2 x 2/CU
     // (profiles/r3_ab_dense_shape_10M.txt)
     // (PSG_DENSE_UNROLL / PSG_DENSE_BPC, when set, still win: A/B runs)
+    // Round 4: the same 2048 threads per CU as 4 blocks of 512
+    // (tools/probe_push_small.hip, 10 M floats, 4 interleaved rounds, one
+    // process): Push 19.2 vs 21.5 us, Pull 12.9 vs 13.1 us, an unperturbed
+    // Push+Pull step 26.8 vs 29.2 us (profiles/r4_probe_push_shapes.txt) —
+    // half the workgroups to dispatch and retire on a ~20 us launch.
     static const bool env_u = getenv("PSG_DENSE_UNROLL") != nullptr;
     static const bool env_b = getenv("PSG_DENSE_BPC") != nullptr;
+    static const bool env_k = getenv("PSG_DENSE_BLOCK") != nullptr;
     c.nt = 1;
     if (!env_u) c.unroll = 1;
-    if (!env_b) c.blocks_per_cu = 8;
+    if (!env_b) c.blocks_per_cu = 4;
+    if (!env_k) c.block = 512;
   } else if (store_bytes <= (512ull << 20)) {
     c.nt = 1;
   } else {

@@ -266,3 +266,20 @@ def test_process_mode_refused_ring_falls_back_to_the_socket():
     r = run(exe, "-ns", 2, "-nw", 2, "-procs", 300000, env={"PS_SHM_RING_REFUSE": "1"}, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.count(" ok") == 2
+
+
+def test_hung_process_job_prints_every_threads_stack():
+    """PS_JOB_TIMEOUT_S: a process job still running at the deadline is taken
+    as hung; every node prints the stacks of all its threads (SIGQUIT), then
+    the launcher kills the job and exits 124.  A 3 M-key job with a 1 s limit
+    stands in for a hang."""
+    exe = os.path.join(BIN, "kv_cluster_host")
+    _need(exe)
+    e = dict(os.environ, PS_JOB_TIMEOUT_S="1")
+    r = subprocess.run([exe, "-ns", "2", "-nw", "2", "-procs", "3000000"], capture_output=True, text=True,
+                       timeout=60, env=e)
+    assert r.returncode == 124, r.stderr[-2000:]
+    assert "PS_JOB_TIMEOUT_S=1" in r.stderr
+    # the scheduler, 2 servers and 2 workers each dumped, thread by thread
+    assert r.stderr.count("SIGQUIT: stacks of every thread follow") == 5, r.stderr[-3000:]
+    assert "RunNode" in r.stderr  # frames carry names (-rdynamic)
