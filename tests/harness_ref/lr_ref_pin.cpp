@@ -14,7 +14,10 @@
 // real-valued gradients (only with one worker or async: the merge order is then
 // fixed), PIN_GRAD=dyadic multiples of 1/64 (exact in any merge order).  At the
 // end worker 0 Pulls the model and prints it as one line of hex words:
-//   MODEL <n> <bits of w[0]> <bits of w[1]> ...
+//   MODEL <rank> <n> <bits of w[0]> <bits of w[1]> ...     (every worker)
+// and, with PIN_MODE=gpu, the server's own model (KVServerLRHandle::GetWeight)
+// when the job ends, so a wrong final model can be told apart from a wrong reply:
+//   SERVER_MODEL <n> <bits of w[0]> ...
 // The reference server reads its settings from the environment as LR_ps does:
 // NUM_FEATURE, LEARNING_RATE, SYNC_MODE, USE_ADAM, ITERATION, DATA_DIR.
 // usage: PIN_MODE=ref|gpu PIN_EPOCHS=E PIN_BATCHES=B lr_ref_pin -ns 1 -nw W
@@ -57,29 +60,69 @@ int main(int argc, char* argv[]) {
       lr::InitWeight(w0, 0, total, current);
       const float lr_rate = std::stof(std::string(Environment::GetOrFail("LEARNING_RATE")));
       auto server = new KVServer<float>(0);
-      server->SetDeviceRequestHandle(KVServerLRHandle(w0, lr_rate, Environment::GetInt("SYNC_MODE") == 0,
-                                                      Environment::Get("USE_ADAM") != nullptr, current, false));
-      RegisterExitCallback([server]() { delete server; });
+      KVServerLRHandle handle(w0, lr_rate, Environment::GetInt("SYNC_MODE") == 0,
+                              Environment::Get("USE_ADAM") != nullptr, current, false);
+      server->SetDeviceRequestHandle(handle);
+      RegisterExitCallback([server, handle]() {
+        const std::vector<float> w = handle.GetWeight();
+        std::string line = "SERVER_MODEL " + std::to_string(w.size());
+        char buf[16];
+        for (float x : w) {
+          uint32_t bits;
+          std::memcpy(&bits, &x, 4);
+          std::snprintf(buf, sizeof(buf), " %08x", bits);
+          line += buf;
+        }
+        std::printf("%s\n", line.c_str());
+        std::fflush(stdout);
+        delete server;
+      });
     }
   }
+  // Workers start once the server is fully built.  The reference's LRServer
+  // installs its request handle BEFORE it sizes and initialises weight_
+  // (LRServer.h:68-86: SetRequestHandle, then weight_.resize and InitWeight),
+  // and LR_ps.cpp starts its workers right after ps::Start (LR_ps.cpp:120-124):
+  // with 200,000 features a first BSP round could be applied while InitWeight
+  // was still writing the tail of weight_, which then overwrote the round
+  // there (the GPUTEST_r03 failure).  The barrier closes that
+  // window for both servers of this harness.
+  Barrier(0, kAllNodes);
   if (IsWorker()) {
     KVWorker<float> kv(0, 0);
     const int rank = MyRank();
     std::vector<Key> keys(n);
     for (int i = 0; i < n; ++i) keys[i] = i;
     std::vector<float> w, g(n);
+    // PIN_TRACE=K: worker 0 also prints the last K features of every Pull reply
+    // (the model after each BSP round), so a test can find the round at which a
+    // wrong model first appears:  PULL <epoch> <batch> <first feature> <bits> ...
+    const int trace = Environment::GetIntOrDefault("PIN_TRACE", 0);
     for (int e = 0; e < epochs; ++e) {
       for (int b = 0; b < batches; ++b) {
         kv.Wait(kv.Pull(keys, &w));
         CHECK_EQ(w.size(), (size_t)n);
+        if (trace > 0 && rank == 0) {
+          const int first = n > trace ? n - trace : 0;
+          std::string line = "PULL " + std::to_string(e) + " " + std::to_string(b) + " " + std::to_string(first);
+          char buf[16];
+          for (int i = first; i < n; ++i) {
+            uint32_t bits;
+            std::memcpy(&bits, &w[i], 4);
+            std::snprintf(buf, sizeof(buf), " %08x", bits);
+            line += buf;
+          }
+          std::printf("%s\n", line.c_str());
+          std::fflush(stdout);
+        }
         for (int i = 0; i < n; ++i) g[i] = grad_of(real, rank, e, b, i);
         kv.Wait(kv.Push(keys, g, {}, b == batches - 1 ? 1 : 0));
       }
     }
     Barrier(0, kWorkerGroup);
     kv.Wait(kv.Pull(keys, &w));
-    if (rank == 0) {
-      std::string line = "MODEL " + std::to_string(n);
+    {
+      std::string line = "MODEL " + std::to_string(rank) + " " + std::to_string(n);
       char buf[16];
       for (int i = 0; i < n; ++i) {
         uint32_t bits;

@@ -30,7 +30,7 @@ LR = 0.01
 EPOCHS, BATCHES = 3, 4
 
 
-def _run(tmp_path, mode, nw, n, adam, sync, grad):
+def _run(tmp_path, mode, nw, n, adam, sync, grad, full=False):
     if not os.path.exists(EXE):
         pytest.skip(f"{EXE} not built (needs the reference tree)")
     os.makedirs(os.path.join(tmp_path, "model"), exist_ok=True)
@@ -48,11 +48,19 @@ def _run(tmp_path, mode, nw, n, adam, sync, grad):
     r = subprocess.run([EXE, "-ns", "1", "-nw", str(nw)], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    line = [l for l in r.stdout.splitlines() if l.startswith("MODEL ")]
-    assert len(line) == 1, r.stdout[-2000:]
-    parts = line[0].split()
-    assert int(parts[1]) == n
-    return np.array([int(x, 16) for x in parts[2:]], dtype=np.uint32).view(np.float32)
+    models = {}
+    for l in r.stdout.splitlines():
+        parts = l.split()
+        if parts and parts[0] == "MODEL":
+            assert int(parts[2]) == n
+            models[int(parts[1])] = np.array([int(x, 16) for x in parts[3:]], dtype=np.uint32).view(np.float32)
+        elif parts and parts[0] == "SERVER_MODEL":
+            assert int(parts[1]) == n
+            models["server"] = np.array([int(x, 16) for x in parts[2:]], dtype=np.uint32).view(np.float32)
+    assert sorted(k for k in models if k != "server") == list(range(nw)), r.stdout[-2000:]
+    if full:
+        return models
+    return models[0]
 
 
 def _init_weight(n, seed=0):
@@ -121,7 +129,39 @@ def test_reference_lr_server_three_workers_sgd_equals_the_oracle_replay(tmp_path
 ])
 def test_hbm_lr_handle_equals_the_reference_lr_server(tmp_path, nw, n, adam, sync, grad):
     want = _run(os.path.join(tmp_path, "ref"), "ref", nw, n, adam, sync, grad)
-    got = _run(os.path.join(tmp_path, "gpu"), "gpu", nw, n, adam, sync, grad)
+    models = _run(os.path.join(tmp_path, "gpu"), "gpu", nw, n, adam, sync, grad, full=True)
+    got = models[0]
     bad = np.nonzero(got.view(np.uint32) != want.view(np.uint32))[0]
+    if bad.size and (nw == 1 or grad == "dyadic"):
+        # which side is wrong: both against the oracle's replay (exact here)
+        orc = _oracle_replay(n, nw, adam, sync, grad == "real")
+        nref = int(np.count_nonzero(want.view(np.uint32) != orc.view(np.uint32)))
+        ngpu = int(np.count_nonzero(got.view(np.uint32) != orc.view(np.uint32)))
+        pytest.fail(f"{bad.size} features differ; first {bad[0]}: HBM handle {got[bad[0]]!r} reference LRServer "
+                    f"{want[bad[0]]!r}; against the oracle replay: reference run {nref} differ, HBM run {ngpu} "
+                    f"differ; " + _diagnose(models, want, nw, grad))
     assert bad.size == 0, (f"{bad.size} features differ; first {bad[0]}: HBM handle {got[bad[0]]!r} "
-                           f"reference LRServer {want[bad[0]]!r}")
+                           f"reference LRServer {want[bad[0]]!r}; " + _diagnose(models, want, nw, grad))
+    # every worker's final Pull, and the server's own model, are the reference's
+    for k, m in models.items():
+        assert np.array_equal(m.view(np.uint32), want.view(np.uint32)), f"{k}: " + _diagnose(models, want, nw, grad)
+
+
+def _diagnose(models, want, nw, grad):
+    """Which copies of the model differ from the reference's, where, and — for
+    dyadic gradients — the differences in units of lr/64 next to each BSP
+    round's merged gradient at the first few differing features (a missing or
+    repeated round shows as a row that matches)."""
+    out = []
+    for k, m in sorted(models.items(), key=lambda kv: str(kv[0])):
+        b = np.nonzero(m.view(np.uint32) != want.view(np.uint32))[0]
+        out.append(f"{k}: {b.size} differ" + (f" in [{b[0]}, {b[-1]}]" if b.size else ""))
+    m0 = models[0]
+    b = np.nonzero(m0.view(np.uint32) != want.view(np.uint32))[0]
+    if b.size and grad == "dyadic":
+        for i in b[:4]:
+            d = (float(m0[i]) - float(want[i])) / LR * 64
+            rounds = {(e, bb): int(sum(((i * 7 + r * 3 + e * 5 + bb) % 11) - 5 for r in range(nw)))
+                      for e in range(EPOCHS) for bb in range(BATCHES)}
+            out.append(f"feature {i}: (got - want) = {d:+.3f} lr/64; merged per (epoch, batch): {rounds}")
+    return "; ".join(out)
