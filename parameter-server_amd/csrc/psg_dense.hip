@@ -258,10 +258,12 @@ static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op) {
     // (profiles/r3_ab_dense_shape_10M.txt)
     // (PSG_DENSE_UNROLL / PSG_DENSE_BPC, when set, still win: A/B runs)
     // Round 4: the same 2048 threads per CU as 4 blocks of 512
-    // (tools/probe_push_small.hip, 10 M floats, 4 interleaved rounds, one
-    // process): Push 19.2 vs 21.5 us, Pull 12.9 vs 13.1 us, an unperturbed
-    // Push+Pull step 26.8 vs 29.2 us (profiles/r4_probe_push_shapes.txt) —
-    // half the workgroups to dispatch and retire on a ~20 us launch.
+    // (tools/probe_push_small.hip, 10 M integer-valued floats, 4 interleaved
+    // rounds, one process): Push 21.8 vs 23.0 us, an unperturbed Push+Pull
+    // step 31.3 vs 32.7 us, the best of 11 shapes (profiles/r4_probe_push_shapes.txt)
+    // — half the workgroups to dispatch and retire on a ~20 us launch.  (The
+    // same probe on all-zero buffers ran ~20 % faster for every shape: the
+    // probes and the bench use real values.)
     static const bool env_u = getenv("PSG_DENSE_UNROLL") != nullptr;
     static const bool env_b = getenv("PSG_DENSE_BPC") != nullptr;
     static const bool env_k = getenv("PSG_DENSE_BLOCK") != nullptr;

@@ -121,9 +121,6 @@ template <> struct Elem<PSG_BF16> {
 // grid-strided beyond (cdna_hip_programming.md Guideline 11).
 constexpr int kBlock = 256;
 int max_stream_blocks();
-// Blocks of `block` threads of `kernel` resident on the whole device at once
-// (psg_runtime.hip): the grid cap for a grid-stride kernel above 64 VGPRs.
-unsigned resident_blocks(const void* kernel, int block);
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 

@@ -18,7 +18,6 @@
 //
 // Bytes per feature: merged f32 4 + weight f32 r/w 8 (+ m, v f64 r/w 32 with
 // Adam): HBM-bound, streamed.
-#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -217,7 +216,9 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
     c2 = 1 - std::pow(adam->beta2, iteration + 1);
   }
   const uint64_t units = vec ? (n + 3) / 4 : n;
-  const uint64_t b = (units + kBlock - 1) / kBlock;
+  uint64_t b = (units + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks();
+  const unsigned grid = (unsigned)(b < cap ? (b ? b : 1) : cap);
   const int ve = vec ? 1 : 0;
   // PSG_LR_NT=0/1 forces the policy (sweeps); default: non-temporal when the
   // model's arrays exceed 512 MiB
@@ -232,16 +233,8 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   const bool blk = adam && adam->blocked;
   auto go = [&](auto adam_c, auto zero_c, auto blk_c) {
     constexpr bool A = decltype(adam_c)::value, Z = decltype(zero_c)::value, B = decltype(blk_c)::value;
-    // grid: at most what the device holds at once (resident_blocks: the Adam
-    // forms hold 6 blocks per CU, not the 8 of the streaming cap)
-#define PSG_LR_LAUNCH(G, X)                                                                               \
-  do {                                                                                                    \
-    const uint64_t cap = std::min<uint64_t>((uint64_t)max_stream_blocks(),                               \
-                                            resident_blocks((const void*)k_lr_apply_sum<A, Z, G, B, X>, kBlock)); \
-    const unsigned grid = (unsigned)(b < cap ? (b ? b : 1) : cap);                                        \
-    k_lr_apply_sum<A, Z, G, B, X><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, \
-                                                           ve, ntm);                                      \
-  } while (0)
+#define PSG_LR_LAUNCH(G, X) \
+  k_lr_apply_sum<A, Z, G, B, X><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
     switch (ngrads) {
       case 1: PSG_LR_LAUNCH(1, true); break;
       case 2: PSG_LR_LAUNCH(2, true); break;

@@ -4,9 +4,6 @@
 #include <mutex>
 #include <vector>
 
-#include <map>
-#include <mutex>
-
 #include "psg_internal.h"
 
 namespace psg {
@@ -38,33 +35,6 @@ int max_stream_blocks() {
     cached[dev] = cus * 8;
   }
   return cached[dev];
-}
-
-// Blocks of `block` threads of `kernel` the whole device holds at once
-// (CUs x the occupancy the kernel's registers and LDS allow), cached per kernel.
-// A grid-stride launch larger than this runs its surplus blocks as a second,
-// thinly occupied round after the first: the Adam apply (80 VGPRs, 6 blocks of
-// 256 per CU) launched at 8 blocks per CU spent its tail with 2 blocks per CU.
-unsigned resident_blocks(const void* kernel, int block) {
-  static std::mutex mu;
-  static std::map<std::pair<const void*, int>, unsigned>* cache = new std::map<std::pair<const void*, int>, unsigned>();
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const auto key = std::make_pair(kernel, block * 64 + dev);
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = cache->find(key);
-    if (it != cache->end()) return it->second;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu < 1) {
-    (void)hipGetLastError();
-    per_cu = 1;
-  }
-  const unsigned r = (unsigned)per_cu * (unsigned)(max_stream_blocks() / 8);
-  std::lock_guard<std::mutex> lk(mu);
-  (*cache)[key] = r;
-  return r;
 }
 
 __host__ __device__ inline uint64_t splitmix64(uint64_t x) {

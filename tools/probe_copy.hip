@@ -91,7 +91,13 @@ int main(int argc, char** argv) {
   u32x4 *src = nullptr, *dst = nullptr;
   CK(hipMalloc(&src, bytes));
   CK(hipMalloc(&dst, bytes));
-  CK(hipMemset(src, 1, bytes));
+  // a byte pattern that varies along the buffer (not one repeated value)
+  {
+    std::vector<unsigned char> h(bytes < (64u << 20) ? bytes : (64u << 20));
+    for (size_t i = 0; i < h.size(); ++i) h[i] = (unsigned char)((i * 2654435761u) >> 13);
+    for (uint64_t off = 0; off < bytes; off += h.size())
+      CK(hipMemcpy((char*)src + off, h.data(), std::min<uint64_t>(h.size(), bytes - off), hipMemcpyHostToDevice));
+  }
   CK(hipMemset(dst, 0, bytes));
   CK(hipDeviceSynchronize());
   hipStream_t st;
