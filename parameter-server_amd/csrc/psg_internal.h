@@ -228,12 +228,13 @@ struct psg_store {
 struct psg_adam {
   uint64_t n;
   double lr, beta1, beta2, eps;
-  // the moments of Adam.h:40-41: blocked (default) — one array with, per 128
-  // features, their 128 m then their 128 v values (m; v unused) — or two
-  // arrays of n doubles (PSG_ADAM_BLOCKED=0); 16-B aligned (hipMalloc)
+  // the moments of Adam.h:40-41 in one of psg_lr.hip's layouts: 1 (default)
+  // per 128 features their 128 m then their 128 v values, 2 per 256 features
+  // four 1 KiB runs of the QUAD lane map (both in m; v unused), 0 two arrays of
+  // n doubles; 16-B aligned (hipMalloc)
   double* m;
   double* v;
-  int blocked;
+  int layout;
 };
 
 namespace psg {

@@ -48,27 +48,37 @@ __device__ __forceinline__ void st_nt(V* p, V x, int nt) {
   else *p = x;
 }
 
-// Adam moments, BLK layout (psg_adam.blocked): one array holding, per 128
-// features, their 128 m values then their 128 v values (2 KiB), so a wave's m
-// and v runs for the same features are neighbours in memory — one stream of
-// moment pairs instead of two.  Element accessors for feature i:
+// Adam moments, three layouts (psg_adam.layout):
+//   0      two arrays of n doubles, m and v;
+//   1 BLK  one array holding, per 128 features, their 128 m values then their
+//          128 v values (2 KiB), so a wave's m and v runs for the same features
+//          are neighbours in memory — one stream of moment pairs instead of two;
+//   2 QUAD one array holding, per 256 features (one wave tile of the QUAD lane
+//          map: lane l owns features 4l..4l+3), four 1 KiB runs — the m of
+//          features (4l, 4l+1) at lane offset 16 l, then the m of (4l+2, 4l+3),
+//          then the same two for v — so every moment load and store of a wave is
+//          one contiguous 1 KiB run with 16 B a lane, as are its f32 loads.
+// Element accessors for feature i:
 __device__ __forceinline__ uint64_t blk_m(uint64_t i) { return (i >> 7) * 256 + (i & 127); }
 __device__ __forceinline__ uint64_t blk_v(uint64_t i) { return (i >> 7) * 256 + 128 + (i & 127); }
-// the m and v of feature i (BLK: the one blocked array m)
-template <bool BLK>
-__device__ __forceinline__ double* mom_m(double* m, uint64_t i) {
-  return BLK ? m + blk_m(i) : m + i;
+__device__ __forceinline__ uint64_t quad_m(uint64_t i) {
+  return (i >> 8) * 512 + 128 * ((i >> 1) & 1) + 2 * ((i & 255) >> 2) + (i & 1);
 }
-template <bool BLK>
+__device__ __forceinline__ uint64_t quad_v(uint64_t i) { return quad_m(i) + 256; }
+template <int LAY>
+__device__ __forceinline__ double* mom_m(double* m, uint64_t i) {
+  return LAY == 2 ? m + quad_m(i) : LAY == 1 ? m + blk_m(i) : m + i;
+}
+template <int LAY>
 __device__ __forceinline__ double* mom_v(double* m, double* v, uint64_t i) {
-  return BLK ? m + blk_v(i) : v + i;
+  return LAY == 2 ? m + quad_v(i) : LAY == 1 ? m + blk_v(i) : v + i;
 }
 
 // MAXG: gradient slots the kernel keeps registers for; EXACT: a round of
 // exactly MAXG frames (1..4: every slot loaded, no run-time frame test, so the
 // registers of absent frames are not held), else up to kMaxGrads (ng at run
-// time).  BLK: the moments in the blocked layout (m is the one array, v unused).
-template <bool ADAM, bool ZERO, int MAXG, bool BLK, bool EXACT>
+// time).  LAY: the moment layout (1, 2: m is the one array, v unused).
+template <bool ADAM, bool ZERO, int MAXG, int LAY, bool EXACT>
 __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Grads g, int ng, uint64_t n,
                                                       float lr, double* __restrict__ m,
                                                       double* __restrict__ v, double alr, double b1,
@@ -93,6 +103,54 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
 #pragma unroll
       for (int e = 0; e < 4; ++e) wv[e] = (float)((double)wv[e] - (double)(lr * s[e]));
       st_nt(reinterpret_cast<u32x4*>(w + 4 * j), __builtin_bit_cast(u32x4, wv), nt);
+    }
+  } else if constexpr (LAY == 2) {
+    // Adam, QUAD: lane unit j owns features 4j..4j+3 (16-B f32 loads, one
+    // 1 KiB run a wave instruction on every stream); T wave tiles per
+    // iteration as below
+    constexpr int T = EXACT ? 2 : 1;
+    const uint64_t nu = vec ? n / 256 * 64 : 0;
+    done = nu * 4;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * kBlock * T + threadIdx.x; j0 < nu; j0 += stride * T) {
+      f32x4 x[T][MAXG], wv[T];
+      f64x2 mo[T][4];  // m(4l, 4l+1), m(4l+2, 4l+3), v(4l, 4l+1), v(4l+2, 4l+3)
+      uint64_t jq[T], mb[T];
+      bool in[T];
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const uint64_t j = j0 + (uint64_t)t * kBlock;
+        in[t] = j < nu;
+        jq[t] = in[t] ? j : j0;  // a tile past the end repeats the first, unwritten
+        mb[t] = (jq[t] >> 6) * 512 + 2 * (jq[t] & 63);
+#pragma unroll
+        for (int k = 0; k < MAXG; ++k)
+          if (EXACT || k < ng)
+            x[t][k] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(g.p[k]) + jq[t]));
+        wv[t] = __builtin_bit_cast(f32x4, ld_nt(reinterpret_cast<const u32x4*>(w) + jq[t], nt));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mo[t][r] = ld_nt(reinterpret_cast<const f64x2*>(m + mb[t] + 128 * r), nt);
+      }
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        f32x4 s = ZERO ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} + x[t][0] : x[t][0];
+#pragma unroll
+        for (int k = 1; k < MAXG; ++k)
+          if (EXACT || k < ng) s = s + x[t][k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double gr = (double)(lr * s[e]);
+          const double mi = b1 * mo[t][e >> 1][e & 1] + (1.0 - b1) * gr;
+          const double vi = b2 * mo[t][2 + (e >> 1)][e & 1] + (1.0 - b2) * gr * gr;
+          mo[t][e >> 1][e & 1] = mi;
+          mo[t][2 + (e >> 1)][e & 1] = vi;
+          wv[t][e] = (float)((double)wv[t][e] - alr * (mi / c1) / (sqrt(vi / c2) + eps));
+        }
+        if (in[t]) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st_nt(reinterpret_cast<f64x2*>(m + mb[t] + 128 * r), mo[t][r], nt);
+          st_nt(reinterpret_cast<u32x4*>(w) + jq[t], __builtin_bit_cast(u32x4, wv[t]), nt);
+        }
+      }
     }
   } else {
     // Adam: 256 features per wave, lane l owning features 2l, 2l+1 of each
@@ -129,13 +187,13 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
             for (int h = 0; h < 2; ++h)
               x[t][k][h] = __builtin_bit_cast(
                   f32x2, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g.p[k] + f0[t] + 128 * h)));
-        // the moment pairs of features f0 + 128 h (BLK: group 2U + h of the
-        // blocked array, U = f0 / 256, at lane offset f0 % 128)
+        // the moment pairs of features f0 + 128 h (layout 1: group 2U + h of
+        // the blocked array, U = f0 / 256, at lane offset f0 % 128)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           wv[t][h] = __builtin_bit_cast(f32x2, ld_nt(reinterpret_cast<const u32x2*>(w + f0[t] + 128 * h), nt));
-          mm[t][h] = ld_nt(reinterpret_cast<const f64x2*>(mom_m<BLK>(m, f0[t] + 128 * h)), nt);
-          vv[t][h] = ld_nt(reinterpret_cast<const f64x2*>(mom_v<BLK>(m, v, f0[t] + 128 * h)), nt);
+          mm[t][h] = ld_nt(reinterpret_cast<const f64x2*>(mom_m<LAY>(m, f0[t] + 128 * h)), nt);
+          vv[t][h] = ld_nt(reinterpret_cast<const f64x2*>(mom_v<LAY>(m, v, f0[t] + 128 * h)), nt);
         }
       }
 #pragma unroll
@@ -156,8 +214,8 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
             wv[t][h][e] = (float)((double)wv[t][h][e] - alr * (mi / c1) / (sqrt(vi / c2) + eps));
           }
           if (in[t]) {
-            st_nt(reinterpret_cast<f64x2*>(mom_m<BLK>(m, f0[t] + 128 * h)), mm[t][h], nt);
-            st_nt(reinterpret_cast<f64x2*>(mom_v<BLK>(m, v, f0[t] + 128 * h)), vv[t][h], nt);
+            st_nt(reinterpret_cast<f64x2*>(mom_m<LAY>(m, f0[t] + 128 * h)), mm[t][h], nt);
+            st_nt(reinterpret_cast<f64x2*>(mom_v<LAY>(m, v, f0[t] + 128 * h)), vv[t][h], nt);
             st_nt(reinterpret_cast<u32x2*>(w + f0[t] + 128 * h), __builtin_bit_cast(u32x2, wv[t][h]), nt);
           }
         }
@@ -169,8 +227,8 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
     for (int k = 1; k < ng; ++k) s = s + g.p[k][i];
     double grad = (double)(lr * s);
     if constexpr (ADAM) {
-      double* mi_p = BLK ? m + blk_m(i) : m + i;
-      double* vi_p = BLK ? m + blk_v(i) : v + i;
+      double* mi_p = mom_m<LAY>(m, i);
+      double* vi_p = mom_v<LAY>(m, v, i);
       const double mi = b1 * *mi_p + (1.0 - b1) * grad;
       const double vi = b2 * *vi_p + (1.0 - b2) * grad * grad;
       *mi_p = mi;
@@ -206,10 +264,10 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   if (adam) {
     PSG_REQUIRE(adam_off <= adam->n && n <= adam->n - adam_off, PSG_ERR_RANGE,
                 "LR apply: Adam state holds %llu features", (unsigned long long)adam->n);
-    PSG_REQUIRE(!adam->blocked || adam_off == 0, PSG_ERR_INVALID, "LR apply: blocked Adam state at an offset");
-    m = adam->m + (adam->blocked ? 0 : adam_off);
-    v = adam->blocked ? nullptr : adam->v + adam_off;
-    vec = vec && aligned16(m) && (adam->blocked || aligned16(v));
+    PSG_REQUIRE(adam->layout == 0 || adam_off == 0, PSG_ERR_INVALID, "LR apply: interleaved Adam state at an offset");
+    m = adam->m + (adam->layout ? 0 : adam_off);
+    v = adam->layout ? nullptr : adam->v + adam_off;
+    vec = vec && aligned16(m) && (adam->layout || aligned16(v));
     // the two bias corrections of Adam.h:31-32, with the host libm pow the
     // reference calls
     c1 = 1 - std::pow(adam->beta1, iteration + 1);
@@ -230,9 +288,10 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   const int ntm = nt_env >= 0 ? (nt_env ? 1 : 0) : (state_bytes > (512ull << 20) ? 1 : 0);
   const double alr = adam ? adam->lr : 0, b1 = adam ? adam->beta1 : 0, b2 = adam ? adam->beta2 : 0,
                eps = adam ? adam->eps : 0;
-  const bool blk = adam && adam->blocked;
-  auto go = [&](auto adam_c, auto zero_c, auto blk_c) {
-    constexpr bool A = decltype(adam_c)::value, Z = decltype(zero_c)::value, B = decltype(blk_c)::value;
+  const int lay = adam ? adam->layout : 0;
+  auto go = [&](auto adam_c, auto zero_c, auto lay_c) {
+    constexpr bool A = decltype(adam_c)::value, Z = decltype(zero_c)::value;
+    constexpr int B = decltype(lay_c)::value;
 #define PSG_LR_LAUNCH(G, X) \
   k_lr_apply_sum<A, Z, G, B, X><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
     switch (ngrads) {
@@ -246,17 +305,18 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (adam && from_zero) {
-    if (blk) go(T_{}, T_{}, T_{});
-    else go(T_{}, T_{}, F_{});
-  } else if (adam) {
-    if (blk) go(T_{}, F_{}, T_{});
-    else go(T_{}, F_{}, F_{});
-  } else if (from_zero) {
-    go(F_{}, T_{}, F_{});
-  } else {
-    go(F_{}, F_{}, F_{});
-  }
+  using L0 = std::integral_constant<int, 0>;
+  using L1 = std::integral_constant<int, 1>;
+  using L2 = std::integral_constant<int, 2>;
+  auto go_adam = [&](auto zero_c) {
+    if (lay == 2) go(T_{}, zero_c, L2{});
+    else if (lay == 1) go(T_{}, zero_c, L1{});
+    else go(T_{}, zero_c, L0{});
+  };
+  if (adam && from_zero) go_adam(T_{});
+  else if (adam) go_adam(F_{});
+  else if (from_zero) go(F_{}, T_{}, L0{});
+  else go(F_{}, F_{}, L0{});
   PSG_HIP(hipGetLastError());
   return PSG_OK;
 }
@@ -278,15 +338,18 @@ int psg_adam_create(uint64_t n, double learning_rate, double beta1, double beta2
   a->beta1 = beta1;
   a->beta2 = beta2;
   a->eps = epsilon;
-  // PSG_ADAM_BLOCKED=0: m and v as two arrays (A/B); default the blocked layout
-  static const int blocked = [] {
-    const char* e = getenv("PSG_ADAM_BLOCKED");
-    return e ? (atoi(e) != 0) : 1;
+  // PSG_ADAM_LAYOUT=0/1/2 (A/B; PSG_ADAM_BLOCKED=0 is layout 0): the moment
+  // layout of k_lr_apply_sum, read at every create (tests switch it); default 1
+  const int layout = [] {
+    const char* e = getenv("PSG_ADAM_LAYOUT");
+    if (e) return atoi(e) == 2 ? 2 : atoi(e) == 0 ? 0 : 1;
+    const char* b = getenv("PSG_ADAM_BLOCKED");
+    return b && atoi(b) == 0 ? 0 : 1;
   }();
-  a->blocked = blocked;
+  a->layout = layout;
   hipError_t e;
-  if (blocked) {
-    const uint64_t words = (n + 127) / 128 * 256;
+  if (layout) {
+    const uint64_t words = layout == 2 ? (n + 255) / 256 * 512 : (n + 127) / 128 * 256;
     e = hipMalloc((void**)&a->m, words * sizeof(double));
     if (e == hipSuccess) e = hipMemset(a->m, 0, words * sizeof(double));
   } else {

@@ -50,10 +50,15 @@ def device():
     yield
 
 
-@pytest.mark.parametrize("adam", [False, True])
+# layout: None = SGD; 0/1/2 = Adam with that moment layout (psg_lr.hip:
+# two arrays, blocked per 128 features, the QUAD runs per 256)
+@pytest.mark.parametrize("layout", [None, 1, 0, 2])
 @pytest.mark.parametrize("n,ng,from_zero", [(100003, 1, False), (100003, 4, True), (4096, 16, True),
-                                            (7, 3, True), (262144, 2, False)])
-def test_lr_apply_sum_bitexact(n, ng, from_zero, adam):
+                                            (7, 3, True), (262144, 2, False), (1000, 5, True)])
+def test_lr_apply_sum_bitexact(n, ng, from_zero, layout, monkeypatch):
+    adam = layout is not None
+    if adam:
+        monkeypatch.setenv("PSG_ADAM_LAYOUT", str(layout))
     rng = np.random.default_rng(n + ng)
     w0 = rng.uniform(-0.5, 0.5, n).astype(np.float32)
     st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
@@ -214,14 +219,16 @@ def test_xgmi_lr_push_multiprocess(world, adam):
 LRG = np.load(os.path.join(ROOT, "tests", "golden", "lr_ref.npz"))
 
 
+@pytest.mark.parametrize("layout", [1, 2])
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("case", [str(c) for c in LRG["cases"]])
-def test_lr_apply_matches_the_reference_adam(case, fused):
+def test_lr_apply_matches_the_reference_adam(case, fused, layout, monkeypatch):
     """psg_lr_apply (the merged frame) and psg_lr_apply_sum (the merge fused in)
     against rounds computed by the REFERENCE's own Adam (tests/src/Adam.h,
     compiled where it lies, inside LRServer's apply loop; fixture
     tests/golden/make_lr_golden.py): bit for bit, round by round, SGD and Adam,
-    repeated and skipped iterations."""
+    repeated and skipped iterations; the Adam moments in two layouts."""
+    monkeypatch.setenv("PSG_ADAM_LAYOUT", str(layout))
     w0 = LRG[f"{case}_w0"]
     n = len(w0)
     lr = float(LRG[f"{case}_lr"][0])
