@@ -909,6 +909,12 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         if getattr(backend, "store_extra", 0):
             res["config"]["store_keys"] = (f"{backend.store_extra + 1} x the request's: the request is every "
                                            f"{backend.store_extra + 1}-th store key (PSG_BENCH_STORE_EXTRA)")
+            # the least HBM a Push at this density can move per request key:
+            # its key 8 + value 4, the store keys its windows span 8 (e + 1),
+            # and the 4-B store values of every line it touches, read and
+            # written (whole 64-B lines while 4 (e + 1) <= 64)
+            e1 = backend.store_extra + 1
+            res["config"]["push_min_bytes_per_key"] = 12 + 8 * e1 + 2 * min(4 * e1, 64)
         if paths["ident"] > 0 and paths["notident"] == 0:
             kname = ("SORTED-store Push: k_ident_check + k_ident_apply (identity request: the key "
                      "list is the stretch K[D, D + n) of the store's keys, D from its first tile's "
@@ -922,7 +928,8 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "cached per key array; requests in flight, each reporting "
                      "completion and flags in one kernel-written word; one "
                      "server, so no slicer pass)")
-        res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args, kname, vb)
+        res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args, kname, vb,
+                                   store_extra=getattr(backend, "store_extra", 0))
         res["pull_roofline_frac"] = round(24 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
@@ -957,19 +964,23 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
     return res
 
 
-def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int) -> dict:
+def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra: int = 0) -> dict:
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed PMC summaries (tools/pmc_summary.py):
-    # the one measured on this kernel at these algorithmic bytes, if any
+    # the one measured on this kernel at these algorithmic bytes and on this
+    # store density (store_extra: store keys between request keys), if any
     traffic, source = None, None
     import glob
-    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    files += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")))
+    for pmc in files:
         try:
             d = json.load(open(pmc))
         except Exception:
             continue
         names = [k.split("<")[0].strip() for k in str(d.get("kernel", "")).split("|")]
-        if d.get("alg_bytes_per_launch") == alg_bytes and names and all(n in kernel for n in names):
+        if (d.get("alg_bytes_per_launch") == alg_bytes and d.get("store_extra", 0) == store_extra and names
+                and all(n in kernel for n in names)):
             traffic = d.get("hbm_bytes_per_launch")
             source = os.path.relpath(pmc, ROOT)
             break
