@@ -43,6 +43,11 @@ for _p in (os.path.join(ROOT, "parameter-server_amd", "python"), os.path.join(RO
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+# The markers that time kernels record without the system-scope release fence
+# (psg_event_create_timing, hipEventDisableSystemFence: "can improve the
+# accuracy of timing measurements by avoiding the cost of cache writeback and
+# invalidation", hip_runtime_api.h); PSG_BENCH_EVENTS=fence for default events
+TIMING_EVENTS = os.environ.get("PSG_BENCH_EVENTS", "timing") != "fence"
 PUSH_ACCESSES = 3      # read vals + read store + write store
 PULL_ACCESSES = 2      # read store + write out
 
@@ -559,7 +564,7 @@ class GpuBackend:
             self.pull()
 
     def new_event(self):
-        return self.p.Event()
+        return self.p.Event(timing=TIMING_EVENTS)
 
     def record(self, e):
         e.record(self.stream)
@@ -655,14 +660,14 @@ class GpuBackend:
         # does not move them.  Back-to-back Pushes alone run ~10 % slower on
         # this store (measured: 0.69 vs 0.785 of HBM) and are reported beside.
         import statistics
-        ev = [p.Event() for _ in range(2 * iters + 1)]
+        ev = [p.Event(timing=TIMING_EVENTS) for _ in range(2 * iters + 1)]
         ev[0].record(self.stream)
         for i in range(iters):
             st.handle(p.PUSH, None, v, None, n, stream=self.stream)
             ev[2 * i + 1].record(self.stream)
             st.handle(p.PULL, None, None, o, n, stream=self.stream)
             ev[2 * i + 2].record(self.stream)
-        eb = [p.Event() for _ in range(iters + 1)]
+        eb = [p.Event(timing=TIMING_EVENTS) for _ in range(iters + 1)]
         eb[0].record(self.stream)
         for i in range(iters):
             st.handle(p.PUSH, None, v, None, n, stream=self.stream)
@@ -684,7 +689,7 @@ class GpuBackend:
         for unroll, bpc in ((1, 4), (2, 2), (4, 2), (4, 3), (8, 2)):
             for _ in range(2):
                 p.copy(o, v, n * 4, unroll, bpc, stream=self.stream)
-            ec = [p.Event() for _ in range(11)]
+            ec = [p.Event(timing=TIMING_EVENTS) for _ in range(11)]
             ec[0].record(self.stream)
             for i in range(10):
                 p.copy(o, v, n * 4, unroll, bpc, stream=self.stream)
@@ -693,7 +698,7 @@ class GpuBackend:
             copy_shapes[f"U{unroll}x{bpc}/CU"] = statistics.median(ec[i].elapsed_ms(ec[i + 1]) for i in range(10))
         best_shape = min(copy_shapes, key=copy_shapes.get)
         copy_ms = copy_shapes[best_shape]
-        em = [p.Event() for _ in range(11)]
+        em = [p.Event(timing=TIMING_EVENTS) for _ in range(11)]
         for _ in range(2):
             p.memcpy_d2d(o, v, n * 4, stream=self.stream)
         em[0].record(self.stream)
@@ -961,6 +966,8 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)
     res["runtime_libs"] = mapped_runtime_libs()
+    res["event_markers"] = ("timing-only (hipEventDisableSystemFence)" if TIMING_EVENTS
+                            else "default (system-scope fence at each record)")
     return res
 
 

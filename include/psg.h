@@ -118,6 +118,13 @@ int psg_stream_create(psg_stream* stream);
 int psg_stream_destroy(psg_stream stream);
 int psg_stream_sync(psg_stream stream);
 int psg_event_create(psg_event* ev);
+/* An event for timing only (bench.py's markers): its record skips the
+   system-scope release fence (hipEventDisableSystemFence), so a marker between
+   two launches does not write back and invalidate the caches — the cost that
+   made an event-timed launch read ~2 us longer than rocprof's kernel time.
+   Elapsed times are valid once the stream has been synchronised; do not use
+   it to hand data to the host or another device. */
+int psg_event_create_timing(psg_event* ev);
 int psg_event_destroy(psg_event ev);
 int psg_event_record(psg_event ev, psg_stream stream);
 int psg_event_sync(psg_event ev);

@@ -275,7 +275,17 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   }
   const uint64_t units = vec ? (n + 3) / 4 : n;
   uint64_t b = (units + kBlock - 1) / kBlock;
-  const uint64_t cap = (uint64_t)max_stream_blocks();
+  // 2 blocks of 256 per CU, grid-striding: at 64 M features SGD 0.87 / 0.81
+  // (1 / 4 frames) and Adam 0.66 / 0.66 of 8 TB/s, against 0.77-0.83 / 0.69-0.76
+  // and 0.64 / 0.65 with 8 per CU; 1 per CU starves SGD of loads in flight
+  // (0.57), 3 and 4 sit between; no difference at 10 M features (two
+  // interleaved rounds each, profiles/r4_ab_lr_bpc.txt).  PSG_LR_BPC=k: k per CU.
+  static const int bpc = [] {
+    const char* e = getenv("PSG_LR_BPC");
+    const int k = e ? atoi(e) : 0;
+    return k >= 1 && k <= 16 ? k : 2;
+  }();
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 8 * bpc;
   const unsigned grid = (unsigned)(b < cap ? (b ? b : 1) : cap);
   const int ve = vec ? 1 : 0;
   // PSG_LR_NT=0/1 forces the policy (sweeps); default: non-temporal when the

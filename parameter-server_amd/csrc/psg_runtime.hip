@@ -288,6 +288,13 @@ int psg_event_create(psg_event* ev) {
   *ev = (psg_event)e;
   return PSG_OK;
 }
+int psg_event_create_timing(psg_event* ev) {
+  PSG_REQUIRE(ev, PSG_ERR_INVALID, "psg_event_create_timing: null out");
+  hipEvent_t e;
+  PSG_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  *ev = (psg_event)e;
+  return PSG_OK;
+}
 int psg_event_destroy(psg_event ev) {
   if (ev) PSG_HIP(hipEventDestroy((hipEvent_t)ev));
   return PSG_OK;

@@ -37,7 +37,7 @@ EXPORTS = [
     "psg_get_device", "psg_device_sync", "psg_enable_peer_access", "psg_malloc", "psg_free", "psg_host_alloc",
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
     "psg_memset", "psg_copy", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
-    "psg_event_create", "psg_event_destroy", "psg_event_record", "psg_event_sync",
+    "psg_event_create", "psg_event_create_timing", "psg_event_destroy", "psg_event_record", "psg_event_sync",
     "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear", "psg_store_counters",
@@ -99,6 +99,7 @@ def lib() -> C.CDLL:
             "psg_copy": ([vp, vp, u64, i32, i32, vp], i32),
             "psg_stream_create": ([C.POINTER(vp)], i32), "psg_stream_destroy": ([vp], i32),
             "psg_stream_sync": ([vp], i32), "psg_event_create": ([C.POINTER(vp)], i32),
+            "psg_event_create_timing": ([C.POINTER(vp)], i32),
             "psg_event_destroy": ([vp], i32), "psg_event_record": ([vp, vp], i32),
             "psg_event_sync": ([vp], i32),
             "psg_event_elapsed_ms": ([vp, vp, C.POINTER(f32)], i32),
@@ -232,9 +233,12 @@ def _s(stream) -> int | None:
 
 
 class Event:
-    def __init__(self):
+    """A HIP event; ``timing=True``: a timing-only marker (psg_event_create_timing,
+    no system-scope fence at its record)."""
+
+    def __init__(self, timing: bool = False):
         self.handle = C.c_void_p(None)
-        _call("psg_event_create", C.byref(self.handle))
+        _call("psg_event_create_timing" if timing else "psg_event_create", C.byref(self.handle))
 
     def record(self, stream=None) -> None:
         _call("psg_event_record", self.handle, _s(stream))

@@ -6,7 +6,7 @@ merge the round's ng gradient frames from 0 in arrival order, then
 weight -= lr * merge (SGD) or the Adam step (tests/src/Adam.h:28-34).
 Algorithmic HBM bytes per feature: 4 per gradient frame + weight read/write 8,
 + Adam's f64 moments m and v read/write 32.  HIP-event medians over 20
-launches on the kernel's stream.
+launches on the kernel's stream (timing-only markers: psg_event_create_timing).
 usage: bench_lr.py [N_FEATURES ...]      default 10000000 67108864
 Writes one JSON line per case and gpurun_out/bench_lr.json.
 """
@@ -33,7 +33,7 @@ def case(n, ng, adam, reps=20):
     for _ in range(3):
         psg.lr_apply_sum(w, grads, n, 0.01, a, it, stream=s)
         it += 1
-    ev = [psg.Event() for _ in range(reps + 1)]
+    ev = [psg.Event(timing=True) for _ in range(reps + 1)]  # timing-only markers, as bench.py
     ev[0].record(s)
     for i in range(reps):
         psg.lr_apply_sum(w, grads, n, 0.01, a, it, stream=s)

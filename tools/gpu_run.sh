@@ -13,6 +13,7 @@
 #   trace    kernel trace of the keyed bench: durations and the idle gaps between
 #            launches (tools/trace_gaps.py)
 #   pmcki / pmckip  PMC traffic of the identity keyed Push (check + apply) / Pull
+#   lr       LR apply roofline (tools/bench_lr.py, 10 M and 64 M features) + its rocprof stats
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
 #            (tools/pmc_targets.py, two passes each)
 set -u
@@ -49,6 +50,10 @@ for st in "$@"; do
           step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
           step 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_w_$st.log 2>&1; echo "$st write rc=$?"
           python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" 10000000 gpurun_out/$out $per ;;
+    lr)   step 300 python3 tools/bench_lr.py 10000000 67108864 > gpurun_out/bench_lr.jsonl 2> gpurun_out/bench_lr.err; echo "lr rc=$?"; cat gpurun_out/bench_lr.jsonl
+          rm -rf gpurun_out/prof_lr
+          step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lr -o run --output-format csv -- python3 tools/bench_lr.py 67108864 > gpurun_out/prof_lr.log 2>&1; echo "proflr rc=$?"
+          cut -c1-160 gpurun_out/prof_lr/run_kernel_stats.csv | head -8 ;;
     pmcpull|pmcadam)
           if [ "$st" = pmcpull ]; then tg=pull256; ks="k_dense_vec<0, 2,"; keys=268435456; per=8; out=pmc_pull256_traffic.json
           else tg=adam64; ks="k_lr_apply_sum<true"; keys=67108864; per=56; out=pmc_lr_adam64_traffic.json; fi

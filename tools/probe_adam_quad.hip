@@ -238,6 +238,10 @@ int main(int argc, char** argv) {
       {"pair T1 4/CU", 4, [&](int g) { k_pair<1><<<g, 256>>>(p); }},
       {"pair T2 4/CU", 4, [&](int g) { k_pair<2><<<g, 256>>>(p); }},
       {"pair T2 2/CU", 2, [&](int g) { k_pair<2><<<g, 256>>>(p); }},
+      {"pair T2 1/CU", 1, [&](int g) { k_pair<2><<<g, 256>>>(p); }},
+      {"pair T1 2/CU", 2, [&](int g) { k_pair<1><<<g, 256>>>(p); }},
+      {"pair T4 2/CU", 2, [&](int g) { k_pair<4><<<g, 256>>>(p); }},
+      {"pair T4 1/CU", 1, [&](int g) { k_pair<4><<<g, 256>>>(p); }},
       {"quad T1 8/CU", 8, [&](int g) { k_quad<1><<<g, 256>>>(p); }},
       {"quad T2 8/CU", 8, [&](int g) { k_quad<2><<<g, 256>>>(p); }},
       {"quad T2 4/CU", 4, [&](int g) { k_quad<2><<<g, 256>>>(p); }},
