@@ -267,12 +267,24 @@ static DenseCfg dense_cfg_for_size(uint64_t store_bytes, int op) {
     static const bool env_u = getenv("PSG_DENSE_UNROLL") != nullptr;
     static const bool env_b = getenv("PSG_DENSE_BPC") != nullptr;
     static const bool env_k = getenv("PSG_DENSE_BLOCK") != nullptr;
-    c.nt = 1;
+    // PSG_DENSE_SMALL_NT / PSG_DENSE_MID_NT: this class's Push / the next
+    // class's cache policy bits (A/B)
+    static const int small_nt = [] {
+      const char* e = getenv("PSG_DENSE_SMALL_NT");
+      const int v = e ? atoi(e) : -1;
+      return v >= 0 && v <= 3 ? v : 1;
+    }();
+    c.nt = (op & PSG_PUSH) ? small_nt : 1;
     if (!env_u) c.unroll = 1;
     if (!env_b) c.blocks_per_cu = 4;
     if (!env_k) c.block = 512;
   } else if (store_bytes <= (512ull << 20)) {
-    c.nt = 1;
+    static const int mid_nt = [] {
+      const char* e = getenv("PSG_DENSE_MID_NT");
+      const int v = e ? atoi(e) : -1;
+      return v >= 0 && v <= 3 ? v : 1;
+    }();
+    c.nt = mid_nt;
   } else {
     // past the Infinity Cache, all non-temporal.  Pull (the Pull-only sweep
     // profiles/r1_sweep_pull_256M.json): 1 vector per lane at 4 blocks/CU

@@ -28,7 +28,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // the library's k_dense_vec shape: U vectors per lane, grid stride; request
 // stream non-temporal, store default policy
-template <int U, int BS, bool PUSH>
+template <int U, int BS, bool PUSH, bool SNT = false>
 __global__ __launch_bounds__(BS) void k_op(u32x4* __restrict__ store, const u32x4* __restrict__ vals,
                                            u32x4* __restrict__ out, uint64_t nvec) {
   const uint64_t tile = (uint64_t)BS * U, gs = (uint64_t)gridDim.x * tile;
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(BS) void k_op(u32x4* __restrict__ store, const u32x
       const uint64_t i = b + (uint64_t)u * BS;
       if (i < nvec) {
         if (PUSH) v[u] = __builtin_nontemporal_load(vals + i);
-        s[u] = store[i];
+        s[u] = SNT ? __builtin_nontemporal_load(store + i) : store[i];
       }
     }
 #pragma unroll
@@ -47,7 +47,9 @@ __global__ __launch_bounds__(BS) void k_op(u32x4* __restrict__ store, const u32x
       const uint64_t i = b + (uint64_t)u * BS;
       if (i < nvec) {
         if (PUSH) {
-          store[i] = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, s[u]) + __builtin_bit_cast(f32x4, v[u]));
+          const u32x4 r = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, s[u]) + __builtin_bit_cast(f32x4, v[u]));
+          if (SNT) __builtin_nontemporal_store(r, store + i);
+          else store[i] = r;
         } else {
           __builtin_nontemporal_store(s[u], out + i);
         }
@@ -101,14 +103,14 @@ struct Shape {
   int blocks_per_cu;
 };
 
-template <int U, int BS, bool PUSH, bool CHUNK>
+template <int U, int BS, bool PUSH, bool CHUNK, bool SNT = false>
 void go(u32x4* st, const u32x4* v, u32x4* o, uint64_t nvec, int blocks, hipStream_t s) {
   const uint64_t need = (nvec + (uint64_t)BS * U - 1) / ((uint64_t)BS * U);
   const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)blocks));
   if (CHUNK)
     k_op_chunk<U, BS, PUSH><<<g, BS, 0, s>>>(st, v, o, nvec);
   else
-    k_op<U, BS, PUSH><<<g, BS, 0, s>>>(st, v, o, nvec);
+    k_op<U, BS, PUSH, SNT><<<g, BS, 0, s>>>(st, v, o, nvec);
 }
 
 int main(int argc, char** argv) {
@@ -135,6 +137,9 @@ int main(int argc, char** argv) {
       {"U1 B256 4/CU", go<1, 256, true, false>, go<1, 256, false, false>, 4},
       {"U1 B512 2/CU", go<1, 512, true, false>, go<1, 512, false, false>, 2},
       {"U1 B512 4/CU", go<1, 512, true, false>, go<1, 512, false, false>, 4},
+      {"U1 B512 4/CU store nt", go<1, 512, true, false, true>, go<1, 512, false, false, true>, 4},
+      {"U1 B256 8/CU store nt", go<1, 256, true, false, true>, go<1, 256, false, false, true>, 8},
+      {"U2 B256 2/CU store nt", go<2, 256, true, false, true>, go<2, 256, false, false, true>, 2},
       {"U1 B512 3/CU", go<1, 512, true, false>, go<1, 512, false, false>, 3},
       {"U1 B1024 2/CU", go<1, 1024, true, false>, go<1, 1024, false, false>, 2},
       {"U1 B1024 1/CU", go<1, 1024, true, false>, go<1, 1024, false, false>, 1},
