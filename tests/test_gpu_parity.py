@@ -579,6 +579,76 @@ def test_sorted_window_cache_transitions(dtype):
     np.testing.assert_array_equal(gv.view(NPT[dtype]), ov)
 
 
+@pytest.mark.parametrize("flags", [psg.PUSH, psg.PUSH | psg.PULL])
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F64])
+def test_push_out_of_order_after_an_ascending_prefix(flags, dtype):
+    """A keyed Push / PushPull that ascends for a while and then goes out of
+    order (the validation pass rejects it before any write and the
+    order-preserving path serves it whole, in arrival order).  Bit-exact
+    against the sequential oracle (KVApp.h:446-454) with the disorder at many
+    positions — inside the first 4096-key tile, at tile edges, near the end —
+    the rest repeating keys of the ascending part, absent keys on both sides
+    (a half-populated store), and some requests in flight; the whole store
+    compared after."""
+    rng = np.random.default_rng(4242 + dtype + flags)
+    univ = np.unique(rng.integers(1 << 20, 1 << 62, 300000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, dtype, 0, KMAX, 0)
+    orc = oracle.Store(dtype)
+    half = univ[::2].copy()
+    w = synth(len(half), dtype, 3, 1, -1.0, 1.0)
+    st.handle(psg.PUSH, dev(half), dev(w), None, len(half))
+    orc.handle(oracle.PUSH, half, w, len(half))
+    outs, keep = [], []
+    cuts = [10, 4095, 4096, 4097, 12288, 50000, 99990]
+    for j, cut in enumerate(cuts):
+        n = 100000
+        k = np.sort(rng.choice(univ, n, replace=False))
+        tail = k[cut:].copy()
+        rng.shuffle(tail)
+        k[cut:] = tail
+        k[-3:] = k[:3]  # the rest repeats keys of the prefix
+        v = synth(n, dtype, 50 + j, 1, -1.0, 1.0)
+        out = psg.DeviceBuffer(n * ES[dtype]) if flags & psg.PULL else None
+        dk, dv = dev(k), dev(v)
+        keep.append((dk, dv))  # a request in flight reads them until it is reaped
+        if j % 2:
+            st.handle_async(flags, dk, dv, out, n)
+        else:
+            st.handle(flags, dk, dv, out, n)
+        exp = orc.handle(flags, k, v, n)
+        if out is not None:
+            outs.append((out, exp, j))
+    st.wait()
+    psg.device_sync()
+    for out, exp, j in outs:
+        np.testing.assert_array_equal(out.download(NPT[dtype], len(exp)), exp, err_msg=f"request {j}")
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv.view(NPT[dtype]), ov)
+    assert st.counters()["ordered"] >= len(cuts), st.counters()
+
+
+def test_unsorted_push_with_a_key_outside_between_in_range_ends_leaves_the_store_unchanged():
+    """A key outside the shard between two in-range ends (so the request is
+    also out of order) rejects the whole request: PSG_ERR_RANGE, nothing
+    applied."""
+    rng = np.random.default_rng(77)
+    kb, ke = 1000, 1 << 62
+    univ = np.unique(rng.integers(kb, ke, 50000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, psg.F32, kb, ke, 0)
+    st.handle(psg.PUSH, dev(univ), dev(rng.uniform(-1, 1, len(univ)).astype(np.float32)), None, len(univ))
+    k0, v0 = st.dump()
+    k = univ.copy()
+    k[10] = ke + 7
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(k), dev(np.ones(len(k), np.float32)), None, len(k))
+    assert ei.value.code == 4
+    k1, v1 = st.dump()
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_array_equal(v1, v0)
+
+
 @pytest.mark.parametrize("every", [2, 3, 5, 40])
 def test_sorted_requests_sparse_in_the_store(every):
     """A request that asks for every `every`-th key of a larger store: its
