@@ -577,6 +577,11 @@ class TcpVan : public Van {
   void OnBarrier(const Message& msg);
   void OnGroupBroadcast(const Message& msg);
   std::shared_ptr<Conn> Connect(int id);
+  std::string last_connect_error_;  // the stage and errno of the last Connect that failed (peers_mu_)
+  std::string LastConnectError() {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    return last_connect_error_;
+  }
   int Encode(const Message& msg, const Node& to, std::string* head, std::vector<SVector<char>>* host_frames);
   SVector<char> MapFrame(int sender, const IpcFrame& f, uint64_t bytes);
   SVector<char> MapShmFrame(int sender, const ShmFrame& f, uint64_t bytes);
@@ -721,9 +726,14 @@ void TcpVan::Start(int customer_id) {
     // the scheduler may start after us (local.py starts them in order, but
     // nothing waits): retry the first connection until the deadline
     std::shared_ptr<Conn> c;
+    auto next_note = std::chrono::steady_clock::now() + std::chrono::seconds(5);
     while (!(c = Connect(kScheduler))) {
       CHECK(std::chrono::steady_clock::now() < deadline)
-          << "cannot reach the scheduler at " << sched_host << ":" << sched_port;
+          << "cannot reach the scheduler at " << sched_host << ":" << sched_port << " (" << LastConnectError() << ")";
+      if (std::chrono::steady_clock::now() > next_note) {
+        LOG(WARNING) << "still connecting to the scheduler: " << LastConnectError();
+        next_note += std::chrono::seconds(5);
+      }
       std::this_thread::sleep_for(std::chrono::milliseconds(50));
     }
     Message join;
@@ -946,12 +956,20 @@ std::shared_ptr<Conn> TcpVan::Connect(int id) {
     n = nt->second;
   }
   sockaddr_in sa;
-  if (!Resolve(n.hostname, n.port, &sa)) return nullptr;
-  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-  if (fd < 0) return nullptr;
-  if (::connect(fd, (sockaddr*)&sa, sizeof(sa)) != 0) {
-    ::close(fd);
+  auto failed = [&](const char* stage) {
+    std::string why = std::string(stage) + " " + n.hostname + ":" + std::to_string(n.port) + ": " + std::strerror(errno);
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    last_connect_error_ = std::move(why);
     return nullptr;
+  };
+  if (!Resolve(n.hostname, n.port, &sa)) return failed("resolve");
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0) return failed("socket");
+  if (::connect(fd, (sockaddr*)&sa, sizeof(sa)) != 0) {
+    const int e = errno;
+    ::close(fd);
+    errno = e;
+    return failed("connect");
   }
   Tune(fd);
   auto c = std::make_shared<Conn>();
@@ -968,7 +986,7 @@ std::shared_ptr<Conn> TcpVan::Connect(int id) {
   }
   const uint32_t hello[2] = {kHello, (uint32_t)name.size()};
   if (!WriteAll(fd, hello, sizeof(hello)) || (name.size() && !WriteAll(fd, name.data(), name.size())))
-    return nullptr;  // (c closes fd)
+    return failed("hello to");  // (c closes fd)
   if (c->ring && !RingAccepted(fd)) c->ring.reset();  // the reader could not map it: the socket carries all
   std::lock_guard<std::mutex> lk(peers_mu_);
   auto ins = conns_.emplace(id, c);
@@ -1484,15 +1502,24 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
   dbuf.push_back(0);
   CHECK(mkdtemp(dbuf.data())) << "mkdtemp " << dir;
   dir = dbuf.data();
-  // per-role config files as local.py writes them (local.py:61-85)
-  auto cfg = [&](const char* role) {
-    std::string path = dir + "/config_" + role + ".json";
-    std::ofstream f(path);
-    f << "{\n  \"PS_NUM_SERVER\": " << num_servers << ",\n  \"PS_NUM_WORKER\": " << num_workers
-      << ",\n  \"PS_ROLE\": \"" << role << "\",\n  \"PS_SCHEDULER_URI\": \"127.0.0.1\",\n"
-      << "  \"PS_SCHEDULER_PORT\": " << port << ",\n  \"PS_VAN_TYPE\": \"tcp\"\n}\n";
-    return path;
-  };
+  // per-role config files as local.py writes them (local.py:61-85), each
+  // written once, completely, before any node starts: rewriting a role's file
+  // for every node of that role truncated it under a node already reading it,
+  // which then fell back to the default PS_SCHEDULER_PORT (8000) and retried
+  // a port nobody listens on until the job timed out (the hang
+  // test_dropin_connection_processes[2-3] showed about once in 4-50 launches)
+  auto cfg_path = [&](const char* role) { return dir + "/config_" + role + ".json"; };
+  for (const char* role : {"scheduler", "server", "worker"}) {
+    const std::string path = cfg_path(role), tmp_path = path + ".tmp";
+    {
+      std::ofstream f(tmp_path);
+      f << "{\n  \"PS_NUM_SERVER\": " << num_servers << ",\n  \"PS_NUM_WORKER\": " << num_workers
+        << ",\n  \"PS_ROLE\": \"" << role << "\",\n  \"PS_SCHEDULER_URI\": \"127.0.0.1\",\n"
+        << "  \"PS_SCHEDULER_PORT\": " << port << ",\n  \"PS_VAN_TYPE\": \"tcp\"\n}\n";
+      CHECK(f.good()) << "writing " << tmp_path;
+    }
+    CHECK_EQ(std::rename(tmp_path.c_str(), path.c_str()), 0) << "rename " << tmp_path;
+  }
   char exe[4096];
   ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
   CHECK_GT(n, 0) << "readlink /proc/self/exe";
@@ -1500,7 +1527,7 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
   std::vector<pid_t> pids;
   std::vector<std::string> logs;
   auto spawn = [&](const char* role, int i) {
-    std::vector<std::string> args = {argv[0], cfg(role), dir + "/log_" + role + std::to_string(i) + ".txt", role};
+    std::vector<std::string> args = {argv[0], cfg_path(role), dir + "/log_" + role + std::to_string(i) + ".txt", role};
     for (int k = 1; k < argc; ++k) args.push_back(argv[k]);
     std::vector<char*> av;
     for (auto& a : args) av.push_back(&a[0]);

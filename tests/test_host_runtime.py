@@ -99,6 +99,19 @@ def test_dropin_connection_processes(ns, nw):
     assert r.returncode == 0, r.stderr[-2000:]
 
 
+def test_process_mode_launches_back_to_back():
+    """Process-mode jobs launched back to back (the launcher writes every
+    role's config once, before any node starts: rewriting a role's file per
+    node truncated it under a node already reading it, which then dialled the
+    default scheduler port until the job hung — about once in 4-50 launches of
+    test_connection -ns 2 -nw 3)."""
+    exe = os.path.join(DROPIN, "test_connection")
+    _need(exe)
+    for i in range(40):
+        r = run(exe, "-ns", 2, "-nw", 3, "-procs", timeout=30)
+        assert r.returncode == 0, f"launch {i}: " + r.stderr[-2000:]
+
+
 def test_dropin_simple_app_processes():
     """test_simple_app.cpp counts requests in a process-global `num` and CHECKs
     it equals 100 on every node: that holds only with one node per process."""
