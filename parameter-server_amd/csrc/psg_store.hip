@@ -51,8 +51,8 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // two-pass resolve, the DENSE-keyed check, psg_store_resolve): pinned host ints
 // the kernels set (one store of 1 per wave that saw the condition —
 // idempotent, no atomics), zeroed by the host before the launch and read once
-// a stream-written completion word has appeared (read_flags): the end of the
-// kernel orders its stores before that word.
+// an event recorded behind the launch has completed (read_flags = stream_done:
+// the completed event promises what a stream synchronisation promises).
 // F_WINMISS: a cached window did not match its tile (searched inline).
 enum { F_MISSING = 0, F_WINMISS = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
 // the host-memory completion word after the flags; never zeroed by reset_flags
