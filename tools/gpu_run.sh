@@ -13,6 +13,7 @@
 #   trace    kernel trace of the keyed bench: durations and the idle gaps between
 #            launches (tools/trace_gaps.py)
 #   pmcki / pmckip  PMC traffic of the identity keyed Push (check + apply) / Pull
+#   pmcks    PMC traffic of the key-cached Push on a stretch of slots (k_dense_vec, 12 B/key)
 #   lr       LR apply roofline (tools/bench_lr.py, 10 M and 64 M features) + its rocprof stats
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
 #            (tools/pmc_targets.py, two passes each)
@@ -40,11 +41,12 @@ for st in "$@"; do
     profkc) rm -rf gpurun_out/prof_keyed_cached
           step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_keyed_cached -o run --output-format csv -- python3 bench.py --workload keyed-cached --no-cpu-baseline --steps 20 > gpurun_out/prof_keyed_cached.json 2>&1; echo "profkc rc=$?"
           f=$(find gpurun_out/prof_keyed_cached -name "*kernel_stats.csv" | head -1); cut -c1-160 "$f" | head -8 ;;
-    pmck|pmckc|pmckp|pmcki|pmckip)
+    pmck|pmckc|pmckp|pmcki|pmckip|pmcks)
           if [ "$st" = pmck ]; then wl=keyed; ks="k_validate_windows|k_resolve_apply<0, 1,"; per=28; out=pmc_keyed_push_traffic.json
           elif [ "$st" = pmcki ]; then wl=keyed; ks="k_ident_check|k_ident_apply<0, 1>"; per=28; out=pmc_keyed_ident_push_traffic.json
           elif [ "$st" = pmckip ]; then wl=keyed; ks="k_ident_apply<0, 2>"; per=24; out=pmc_keyed_ident_pull_traffic.json
           elif [ "$st" = pmckp ]; then wl=keyed; ks="k_resolve_apply<0, 2,"; per=24; out=pmc_keyed_pull_traffic.json
+          elif [ "$st" = pmcks ]; then wl=keyed-cached; ks="k_dense_vec<0, 1,"; per=12; out=pmc_keyed_stretch_push_traffic.json
           else wl=keyed-cached; ks="k_slots_vec<0, 1,"; per=16; out=pmc_keyed_cached_push_traffic.json; fi
           rm -rf gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st
           step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
