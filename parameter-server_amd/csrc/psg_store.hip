@@ -1629,7 +1629,22 @@ template <int DT, int OP>
 static void launch_ident(psg_store* s, const uint64_t* q, uint64_t n, const void* vals, void* out, const Win* win,
                          const InflightReq& rec, hipStream_t st) {
   using T = typename Elem<DT>::T;
-  const unsigned g = grid_n(n, (uint64_t)kBlock * 4 * kIdU);
+  // PSG_ID_BPC / PSG_ID_CHECK_BPC (A/B): blocks of 256 per CU of the apply / the
+  // check (default 8, the streaming grid)
+  static const int id_bpc = [] {
+    const char* e = getenv("PSG_ID_BPC");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : 8;
+  }();
+  static const int idc_bpc = [] {
+    const char* e = getenv("PSG_ID_CHECK_BPC");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : 8;
+  }();
+  const unsigned g0 = grid_n(n, (uint64_t)kBlock * 4 * kIdU);
+  const unsigned cus = (unsigned)(max_stream_blocks() / 8);
+  const unsigned g = std::min<unsigned>(g0, cus * (unsigned)id_bpc);
+  const unsigned gc = std::min<unsigned>(g0, cus * (unsigned)idc_bpc);
   // PSG_ID_NT (A/B): bit 0 the store values written non-temporally, bit 1 read so
   static const int id_nt = [] {
     const char* e = getenv("PSG_ID_NT");
@@ -1638,7 +1653,7 @@ static void launch_ident(psg_store* s, const uint64_t* q, uint64_t n, const void
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
                   (aligned16(q) ? 2 : 0) | ((id_nt & 1) ? 4 : 0) | ((id_nt & 2) ? 8 : 0);
   if (OP & PSG_PUSH)
-    k_ident_check<<<g, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->reject_dev, s->seq, vec);
+    k_ident_check<<<gc, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->reject_dev, s->seq, vec);
   Arrival arr;
   arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
   k_ident_apply<DT, OP><<<g, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, (T*)s->vals, (const T*)vals,
