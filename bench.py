@@ -60,6 +60,10 @@ WORKLOADS = {
     # first request resolves the key list once, later ones name it by hash and
     # run on the cached slots (psg_store_handle_slots)
     "keyed-cached": ("f32", 4, 10_000_000, 10_000_000, "configs[3] (key caching)", "configs[3] (key caching)"),
+    # configs[3]'s server side as LRServer runs it in sync mode (LRServer.h:151-178):
+    # one BSP round = merge the nw = 4 workers' gradient frames + the Adam update
+    # (Adam.h:28-34), one kernel (psg_lr_apply_sum); a line of its own (run_lr)
+    "lr": ("f32", 4, 64 << 20, 64 << 20, "LR BSP round", "LR BSP round"),
 }
 # algorithmic HBM bytes per key of one keyed Push on the SORTED store:
 # request key 8 + store key 8 (resolve) + value 4 + store value read/write 8
@@ -971,6 +975,107 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
     return res
 
 
+def run_lr(args) -> dict:
+    """The LR server's sync round on one GPU (configs[3]'s LRServer apply,
+    LRServer.h:151-178 + Adam.h:28-34): `frames` gradient frames merged from 0 in
+    arrival order and the Adam step over `keys` features, one launch of
+    k_lr_apply_sum per step (psg_lr_apply_sum), everything resident in HBM.
+    value = algorithmic HBM bytes per round (4 B per frame + weight 8 + f64
+    moments 32, per feature) / ms_per_step.  Parity: the first 4096 features
+    replayed round by round by the oracle's restatement (bit-exact)."""
+    import numpy as np
+    import psg as p
+    n, frames, lr = args.keys, args.lr_frames, float(np.float32(0.01))
+    p.set_device(0)
+    st = p.Stream()
+    w = p.Store(p.DENSE, p.F32, 0, n, n)
+    init = p.DeviceBuffer(n * 4)
+    init.fill_synth(n, p.F32, args.seed, 1, -0.5, 0.5, st)
+    w.handle(p.PUSH, None, init, None, n, stream=st)
+    grads = [p.DeviceBuffer(n * 4) for _ in range(frames)]
+    for j, g in enumerate(grads):
+        g.fill_synth(n, p.F32, args.seed + 100 + j, 1, -1.0, 1.0, st)
+    adam = p.Adam(n, lr)
+    st.sync()
+    sample = 4096
+    w0 = init.download(np.float32, sample)
+    g0 = [g.download(np.float32, sample) for g in grads]
+    init.free()
+    it = 0
+    for _ in range(args.warmup):
+        p.lr_apply_sum(w, grads, n, 0.01, adam, it, stream=st)
+        it += 1
+    ev = [p.Event(timing=TIMING_EVENTS) for _ in range(args.steps + 1)]
+    st.sync()
+    t0 = time.perf_counter()
+    ev[0].record(st)
+    for i in range(args.steps):
+        p.lr_apply_sum(w, grads, n, 0.01, adam, it, stream=st)
+        it += 1
+        ev[i + 1].record(st)
+    st.sync()
+    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    kernel_ms = sum(ev[i].elapsed_ms(ev[i + 1]) for i in range(args.steps)) / args.steps
+    per = 4 * frames + 8 + 32
+    buf = p.DeviceBuffer(n * 4)
+    w.handle(p.PULL, None, None, buf, n, stream=st)
+    st.sync()
+    got = buf.download(np.float32, sample)
+    buf.free()
+    # the checker: the oracle's restatement of the same rounds on the sample
+    import oracle
+    ref = w0.copy()
+    m, v = np.zeros(sample), np.zeros(sample)
+    for r in range(it):
+        merged = np.zeros(sample, np.float32)
+        for g in g0:
+            merged = (merged + g).astype(np.float32)
+        oracle.lr_apply(ref, merged, 0.01, m, v, lr, 0.9, 0.999, 1e-8, r)
+    bad = int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32)))
+    adam.close()
+    w.close()
+    for g in grads:
+        g.free()
+    gbs = per * n / (ms * 1e-3) / 1e9
+    res = {
+        "metric": "device-resident LR BSP round GB/s (merge + Adam, algorithmic HBM bytes)",
+        "value": round(gbs, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32 merge, f64 Adam", "data": "synthetic (U(-0.5,0.5) weights, U(-1,1) gradients, generated in HBM)",
+        "config": {"workload": f"LR BSP round: {frames} gradient frames merged + Adam over {n} features "
+                               "(configs[3]'s LRServer sync apply, LRServer.h:151-178, Adam.h:28-34)",
+                   "features": n, "frames": frames, "alg_bytes_per_feature": per},
+        "parity_check": bad == 0,
+        "parity_detail": {"sample": sample, "rounds": it, "mismatches": bad,
+                          "oracle": "oracle.lr_apply, bit-exact restatement pinned by tests/golden/lr_ref.npz"},
+        "roofline": roofline(per * n, kernel_ms, args, "k_lr_apply_sum<ADAM> (merge + Adam, one launch)", 4),
+        "event_markers": ("timing-only (hipEventDisableSystemFence)" if TIMING_EVENTS
+                          else "default (system-scope fence at each record)"),
+    }
+    if not args.no_cpu_baseline:
+        # the same round restated in oracle/ on one core, on a bounded sample
+        cn = min(n, args.cpu_lr_features)
+        rng = np.random.default_rng(args.seed)
+        cw = rng.uniform(-0.5, 0.5, cn).astype(np.float32)
+        cg = [rng.uniform(-1, 1, cn).astype(np.float32) for _ in range(frames)]
+        cm, cv = np.zeros(cn), np.zeros(cn)
+        reps = 3
+        t0 = time.perf_counter()
+        for r in range(reps):
+            merged = np.zeros(cn, np.float32)
+            for g in cg:
+                merged = (merged + g).astype(np.float32)
+            oracle.lr_apply(cw, merged, 0.01, cm, cv, lr, 0.9, 0.999, 1e-8, r)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(per * cn * reps / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+                               "kind": "port",
+                               "sample": f"{cn} features x {reps} rounds ({frames} frames merged with numpy f32 adds, "
+                                         f"then oracle.lr_apply's Adam), single thread, {dt:.1f} s",
+                               "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()}}
+    res["runtime_libs"] = mapped_runtime_libs()
+    return res
+
+
 def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra: int = 0) -> dict:
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed PMC summaries (tools/pmc_summary.py):
@@ -1091,6 +1196,9 @@ def main(argv=None) -> None:
     ap.add_argument("--cpu-reps", type=int, default=12)
     ap.add_argument("--cpu-configs0-keys", type=int, default=10_000_000,
                     help="also time configs[0]'s layout at this many keys (0: skip)")
+    ap.add_argument("--lr-frames", type=int, default=4, help="--workload lr: gradient frames per round (nw)")
+    ap.add_argument("--cpu-lr-features", type=int, default=8 << 20,
+                    help="--workload lr: features of the CPU baseline's sample")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1101,6 +1209,11 @@ def main(argv=None) -> None:
     dtype, _, keys1, keysn = WORKLOADS[args.workload][:4]
     if args.keys is None:
         args.keys = keys1 if world == 1 else keysn
+    if args.workload == "lr":
+        if world > 1:
+            raise SystemExit("--workload lr is a one-GPU line (the N > 1 LR round is psg_comm_lr_push)")
+        print(json.dumps(run_lr(args)), flush=True)
+        return
     group = None
     if world > 1:
         from psg_group import SocketGroup

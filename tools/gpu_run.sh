@@ -15,6 +15,7 @@
 #   pmcki / pmckip  PMC traffic of the identity keyed Push (check + apply) / Pull
 #   pmcks    PMC traffic of the key-cached Push on a stretch of slots (k_dense_vec, 12 B/key)
 #   lr       LR apply roofline (tools/bench_lr.py, 10 M and 64 M features) + its rocprof stats
+#   lrb      the bench line of the LR BSP round (bench.py --workload lr) + its rocprof stats
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
 #            (tools/pmc_targets.py, two passes each)
 set -u
@@ -52,6 +53,10 @@ for st in "$@"; do
           step 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_f_$st.log 2>&1; echo "$st fetch rc=$?"
           step 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w_$st -- python3 bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 2 --check 0 > gpurun_out/pmc_w_$st.log 2>&1; echo "$st write rc=$?"
           python3 tools/pmc_summary.py gpurun_out/pmc_f_$st gpurun_out/pmc_w_$st "$ks" 10000000 gpurun_out/$out $per ;;
+    lrb)  step 300 python3 bench.py --workload lr > gpurun_out/bench_lr_line.json 2> gpurun_out/bench_lr_line.err; echo "lrb rc=$?"; cat gpurun_out/bench_lr_line.json; tail -3 gpurun_out/bench_lr_line.err
+          rm -rf gpurun_out/prof_lrb
+          step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lrb -o run --output-format csv -- python3 bench.py --workload lr --no-cpu-baseline > gpurun_out/prof_lrb.log 2>&1; echo "proflrb rc=$?"
+          cut -c1-160 gpurun_out/prof_lrb/run_kernel_stats.csv | head -4 ;;
     lr)   step 300 python3 tools/bench_lr.py 10000000 67108864 > gpurun_out/bench_lr.jsonl 2> gpurun_out/bench_lr.err; echo "lr rc=$?"; cat gpurun_out/bench_lr.jsonl
           rm -rf gpurun_out/prof_lr
           step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lr -o run --output-format csv -- python3 tools/bench_lr.py 67108864 > gpurun_out/prof_lr.log 2>&1; echo "proflr rc=$?"
