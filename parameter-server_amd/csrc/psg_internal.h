@@ -152,6 +152,7 @@ struct InflightReq {
   int want_land;  // a Pull answered when reaped (psg_store_handle): its reply must be in memory then
   int land;       // ... and land_ev[ring] was recorded behind its kernels to say so
   int ident;      // sent as an identity request (k_ident_check / k_ident_apply)
+  int nt;         // threads per block (tile = 4 keys a lane) of its resolve-and-apply launch
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
 }  // namespace psg
@@ -220,6 +221,7 @@ struct psg_store {
     uint32_t ident_fail; // K's generation at which an identity request on this list was not one
     uint32_t ident_ok;   // K's generation at which an identity request on this list completed as one
     uint64_t ident_trial;  // ticket of the identity attempt in flight before either is known (0: none)
+    int nt;              // the block size (tile size / 4) its windows were filled for
   } wc[4];
   uint64_t wc_clock;
   uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters

@@ -1322,13 +1322,21 @@ static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, hipStream
 // 1024).  The tile is 4 keys per lane, so a larger block leaves fewer windows
 // to search (10 M keys: k_tile_windows 11.2 -> 8.8 us from 256 to 512; keyed
 // Push+Pull 606 / 660 / 675 GB/s at 256 / 512 / 1024).
-static int ra_block() {
-  static const int nt = [] {
+// A request sparse in the store (the store holds at least 1.5x as many keys
+// as the request asks for — every other key of a larger store, an LR
+// minibatch) gets 256-thread blocks instead: its tiles' windows span more
+// store keys than they have keys, and smaller windows let 8 blocks per CU
+// stage theirs at once instead of 2 (every 2nd key of a 20 M-key store:
+// keyed Push+Pull 484 against 455-459 GB/s; a request covering its range:
+// 1024 stays ahead, 805 against 790; profiles/r4_ab_ra_block_sparse.txt).
+static int ra_block(const psg_store* s, uint64_t n) {
+  static const int env = [] {
     const char* e = getenv("PSG_RA_BLOCK");
     const int v = e ? atoi(e) : 0;
-    return v == 256 || v == 512 ? v : 1024;
+    return v == 256 || v == 512 || v == 1024 ? v : 0;
   }();
-  return nt;
+  if (env) return env;
+  return 2 * s->size >= 3 * n ? 256 : 1024;
 }
 
 // The window cache entry for request keys (q, n): the entry last filled for
@@ -1594,7 +1602,7 @@ template <int DT, int OP>
 static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void* vals, void* out, Win* win,
                          const InflightReq& rec, hipStream_t st) {
   using T = typename Elem<DT>::T;
-  const int nt = ra_block();
+  const int nt = rec.nt;
   const uint64_t ntiles = (n + (uint64_t)nt * kPerLane - 1) / ((uint64_t)nt * kPerLane);
   // bit 0: request values / replies 16-B aligned; bit 1: request keys 16-B aligned
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
@@ -1664,7 +1672,7 @@ static void launch_ident(psg_store* s, const uint64_t* q, uint64_t n, const void
 template <int DT>
 static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, const void* vals, void* out,
                         hipStream_t st, InflightReq* rec, bool want_land) {
-  const int nt = ra_block();
+  const int nt = ra_block(s, n);
   const uint64_t tile = (uint64_t)nt * kPerLane;
   const uint64_t ntiles = (n + tile - 1) / tile;
   // the window-cache entry (win_entry's choice): requests in flight may share
@@ -1684,6 +1692,15 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   }
   psg_store::WinCache* wc = win_entry(s, q, n, ntiles, st);
   PSG_REQUIRE(wc, PSG_ERR_HIP, "SORTED store: window cache allocation failed");
+  if (wc->nt != nt) {
+    // windows filled for another tile size (the store grew past the sparse
+    // threshold): searched again, and no verdict carried over
+    wc->nt = nt;
+    wc->trusted = 0;
+    wc->strikes = 0;
+    wc->ident_fail = 0;
+    wc->ident_ok = 0;
+  }
   Win* win = static_cast<Win*>(wc->win);
   static const int cache_on = [] {
     const char* e = getenv("PSG_WIN_CACHE");  // 0: always run the search pre-pass (A/B)
@@ -1723,6 +1740,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   rec->wc = (int)(wc - s->wc);
   rec->stream = st;
   rec->ident = ident ? 1 : 0;
+  rec->nt = nt;
   s->counters[ident ? PSG_CTR_IDENT : PSG_CTR_FUSED]++;
   if (ident) {
     switch (op) {

@@ -649,6 +649,52 @@ def test_unsorted_push_with_a_key_outside_between_in_range_ends_leaves_the_store
     np.testing.assert_array_equal(v1, v0)
 
 
+def test_sorted_list_across_the_sparse_threshold():
+    """One key list served while its store grows from exactly its keys to 3x
+    as many: the resolve-and-apply launch switches from 1024- to 256-thread
+    tiles (ra_block: a request sparse in the store), its window-cache entry is
+    searched again for the new tiles, and every request — synchronous and in
+    flight, on both sides of the switch — matches the oracle, as does the whole
+    store after."""
+    rng = np.random.default_rng(2024)
+    univ = np.unique(rng.integers(1 << 20, 1 << 62, 330000, dtype=np.uint64))
+    a = np.sort(rng.choice(univ, 100000, replace=False))
+    rest = np.setdiff1d(univ, a)
+    st = psg.Store(psg.SORTED, psg.F32, 0, KMAX, 0)
+    orc = oracle.Store()
+    dk = dev(a)
+    n = len(a)
+    keep = []
+    for phase in range(2):
+        if phase == 1:  # the store grows past 1.5x the list: the sparse tiles
+            v = rng.uniform(-1, 1, len(rest)).astype(np.float32)
+            st.handle(psg.PUSH, dev(rest), dev(v), None, len(rest))
+            orc.handle(oracle.PUSH, rest, v, len(rest))
+        for j in range(6):
+            flags = [psg.PUSH, psg.PUSH | psg.PULL, psg.PULL][j % 3]
+            v = rng.uniform(-1, 1, n).astype(np.float32)
+            dv = dev(v)
+            out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+            keep.append((dv, out))
+            if j >= 3:
+                st.handle_async(flags, dk, dv if flags & psg.PUSH else None, out, n)
+            else:
+                st.handle(flags, dk, dv if flags & psg.PUSH else None, out, n)
+            exp = orc.handle(flags, a, v if flags & psg.PUSH else None, n)
+            if out is not None:
+                keep.append((out, exp, f"phase {phase} request {j}"))
+        st.wait()
+    psg.device_sync()
+    for item in keep:
+        if len(item) == 3:
+            out, exp, what = item
+            np.testing.assert_array_equal(out.download(np.float32, n), exp, err_msg=what)
+    gk, gv = st.dump()
+    ok, ov = orc.dump()
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv, ov)
+
+
 @pytest.mark.parametrize("every", [2, 3, 5, 40])
 def test_sorted_requests_sparse_in_the_store(every):
     """A request that asks for every `every`-th key of a larger store: its
