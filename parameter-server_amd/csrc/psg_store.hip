@@ -464,7 +464,7 @@ __device__ __forceinline__ void stage_window(uint64_t* sK, const uint64_t* __res
 // CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
 // instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
 // and the 10 M-key Pull took 56 us instead of 40.
-template <int DT, int OP, int NT>
+template <int DT, int OP, int NT, bool SP = false>
 __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
                                                        const uint64_t* __restrict__ K, uint64_t S,
                                                        Win* __restrict__ win, uint32_t gen, uint64_t kb,
@@ -722,7 +722,42 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
     bool vecv = false;
     if constexpr (sizeof(T) == 4)
       vecv = hit[0] && hit[1] && hit[2] && hit[3] && slot[3] == slot[0] + 3 && (slot[0] & 3) == 0;
-    if (vecv) {
+    // (vec & 4, a Push sparse in its store) a lane whose 4 keys lie in one
+    // 32-B aligned span of 8 slots that no other lane writes — its wave
+    // neighbours' keys outside it, and not at a wave's edge, whose neighbour
+    // is another wave's — moves the span as two vectors and writes it back
+    // whole, its other slots unchanged: every line written in full
+    bool span8 = false;
+    uint64_t sbase = 0;
+    f32x4 sa = {}, sb = {};
+    if constexpr (SP && sizeof(T) == 4 && (OP & PSG_PUSH) != 0) {
+      {
+        const uint64_t lo_hit = hit[0] ? slot[0] : hit[1] ? slot[1] : hit[2] ? slot[2] : hit[3] ? slot[3] : ~0ull;
+        const uint64_t hi_hit = hit[3] ? slot[3] : hit[2] ? slot[2] : hit[1] ? slot[1] : hit[0] ? slot[0] : 0ull;
+        const uint32_t plo = __shfl_up((uint32_t)hi_hit, 1, 64), phi = __shfl_up((uint32_t)(hi_hit >> 32), 1, 64);
+        const uint32_t nlo = __shfl_down((uint32_t)lo_hit, 1, 64), nhi = __shfl_down((uint32_t)(lo_hit >> 32), 1, 64);
+        const uint64_t prev_hi = ((uint64_t)phi << 32) | plo, next_lo = ((uint64_t)nhi << 32) | nlo;
+        const int lane = threadIdx.x & 63;
+        sbase = slot[0] & ~7ull;
+        span8 = !vecv && lane != 0 && lane != 63 && hit[0] && hit[1] && hit[2] && hit[3] && slot[3] < sbase + 8 &&
+                sbase + 8 <= S && prev_hi < sbase && next_lo >= sbase + 8;
+      }
+    }
+    if (span8) {
+      if constexpr (sizeof(T) == 4 && (OP & PSG_PUSH) != 0) {
+        sa = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + sbase));
+        sb = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + sbase + 4));
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) {
+          const uint32_t d = (uint32_t)(slot[k] - sbase);
+          T y = sa[0];
+#pragma unroll
+          for (int e = 1; e < 8; ++e)
+            if (d == (uint32_t)e) y = e < 4 ? sa[e & 3] : sb[e & 3];
+          x[k] = y;
+        }
+      }
+    } else if (vecv) {
       if constexpr (sizeof(T) == 4) {
         const f32x4 xv = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + slot[0]));
 #pragma unroll
@@ -741,7 +776,22 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
       if constexpr ((OP & PSG_PUSH) != 0) o[k] = E::add1(x[k], v[k]);
     }
     if constexpr ((OP & PSG_PUSH) != 0) {
-      if (vecv) {
+      if (span8) {
+        if constexpr (sizeof(T) == 4) {
+#pragma unroll
+          for (int k = 0; k < kPerLane; ++k) {
+            const uint32_t d = (uint32_t)(slot[k] - sbase);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (d == (uint32_t)e) {
+                if (e < 4) sa[e & 3] = o[k];
+                else sb[e & 3] = o[k];
+              }
+          }
+          *reinterpret_cast<u32x4*>(V + sbase) = __builtin_bit_cast(u32x4, sa);
+          *reinterpret_cast<u32x4*>(V + sbase + 4) = __builtin_bit_cast(u32x4, sb);
+        }
+      } else if (vecv) {
         if constexpr (sizeof(T) == 4)
           *reinterpret_cast<u32x4*>(V + slot[0]) = __builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]});
       } else {
@@ -1605,8 +1655,13 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
   const int nt = rec.nt;
   const uint64_t ntiles = (n + (uint64_t)nt * kPerLane - 1) / ((uint64_t)nt * kPerLane);
   // bit 0: request values / replies 16-B aligned; bit 1: request keys 16-B aligned
+  // PSG_RA_VECW=1 (A/B): a Push sparse in its store writes whole 8-slot spans
+  static const int vecw = [] {
+    const char* e = getenv("PSG_RA_VECW");
+    return e ? atoi(e) : 0;
+  }();
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
-                  (aligned16(q) ? 2 : 0);
+                  (aligned16(q) ? 2 : 0) | (vecw && aligned16(s->vals) ? 4 : 0);
   const unsigned g = grid_n(ntiles, 1);
   Arrival arr;
   arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
@@ -1615,6 +1670,8 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
       s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8
   if (nt == 1024)
     k_resolve_apply<DT, OP, 1024><<<g, 1024, 0, st>>>(PSG_RA_ARGS);
+  else if (nt == 256 && (vec & 4) && (OP & PSG_PUSH) && sizeof(T) == 4)
+    k_resolve_apply<DT, OP, 256, true><<<g, 256, 0, st>>>(PSG_RA_ARGS);
   else if (nt == 512)
     k_resolve_apply<DT, OP, 512><<<g, 512, 0, st>>>(PSG_RA_ARGS);
   else
