@@ -732,8 +732,13 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
     f32x4 sa = {}, sb = {};
     if constexpr (SP && sizeof(T) == 4 && (OP & PSG_PUSH) != 0) {
       {
-        const uint64_t lo_hit = hit[0] ? slot[0] : hit[1] ? slot[1] : hit[2] ? slot[2] : hit[3] ? slot[3] : ~0ull;
-        const uint64_t hi_hit = hit[3] ? slot[3] : hit[2] ? slot[2] : hit[1] ? slot[1] : hit[0] ? slot[0] : 0ull;
+        // a neighbour bounds the span only through its key next to this
+        // lane's, found: a lane whose key there is absent says nothing about
+        // where the found keys of the lanes beyond it sit (they may fall in
+        // the span), so it disables the span (its first slot reads 0 for the
+        // lane before it, its last all ones for the lane after)
+        const uint64_t lo_hit = hit[0] ? slot[0] : 0ull;
+        const uint64_t hi_hit = hit[3] ? slot[3] : ~0ull;
         const uint32_t plo = __shfl_up((uint32_t)hi_hit, 1, 64), phi = __shfl_up((uint32_t)(hi_hit >> 32), 1, 64);
         const uint32_t nlo = __shfl_down((uint32_t)lo_hit, 1, 64), nhi = __shfl_down((uint32_t)(lo_hit >> 32), 1, 64);
         const uint64_t prev_hi = ((uint64_t)phi << 32) | plo, next_lo = ((uint64_t)nhi << 32) | nlo;
@@ -1655,10 +1660,15 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
   const int nt = rec.nt;
   const uint64_t ntiles = (n + (uint64_t)nt * kPerLane - 1) / ((uint64_t)nt * kPerLane);
   // bit 0: request values / replies 16-B aligned; bit 1: request keys 16-B aligned
-  // PSG_RA_VECW=1 (A/B): a Push sparse in its store writes whole 8-slot spans
+  // a Push sparse in its store (256-thread tiles) writes whole 8-slot spans
+  // where it may (k_resolve_apply<.., SP>): every 2nd key of a 20 M-key store,
+  // Push 112-113 -> 102 us, Push+Pull 488-490 -> 508-510 GB/s; a standalone
+  // probe of that store traffic, 3.5 -> 5.6 TB/s (partly written lines cost
+  // the memory a read-modify-write of their own; profiles/r4_ab_sparse_span.txt).
+  // PSG_RA_VECW=0: never (A/B)
   static const int vecw = [] {
     const char* e = getenv("PSG_RA_VECW");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
                   (aligned16(q) ? 2 : 0) | (vecw && aligned16(s->vals) ? 4 : 0);
