@@ -45,6 +45,7 @@
 namespace psg {
 
 constexpr int kTile = 1024;  // request keys per block tile (4 per lane)
+
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
 // Request flags of the launches that report through the stream (the
@@ -464,8 +465,8 @@ __device__ __forceinline__ void stage_window(uint64_t* sK, const uint64_t* __res
 // CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
 // instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
 // and the 10 M-key Pull took 56 us instead of 40.
-template <int DT, int OP, int NT, bool SP = false>
-__global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
+template <int DT, int OP, int NT, bool SP = false, int WM = 2>
+__global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
                                                        const uint64_t* __restrict__ K, uint64_t S,
                                                        Win* __restrict__ win, uint32_t gen, uint64_t kb,
                                                        uint64_t ke,
@@ -478,7 +479,10 @@ __global__ __launch_bounds__(NT, 8) void k_resolve_apply(const uint64_t* __restr
   using E = Elem<DT>;
   using T = typename E::T;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
-  constexpr uint32_t winN = 2 * NT * kPerLane;          // LDS window of store keys
+  // LDS window of store keys: WM times the tile (2; 4 for a request at most
+  // 2 in 5 of whose store's keys it asks for, whose windows would otherwise
+  // stream through LDS in chunks)
+  constexpr uint32_t winN = WM * NT * kPerLane;
   __shared__ uint64_t sK[winN];
   __shared__ uint64_t sBound[2];
   __shared__ uint32_t s_cond;
@@ -1678,10 +1682,20 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
 #define PSG_RA_ARGS                                                                                     \
   q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end, (T*)s->vals, (const T*)vals, (T*)out, \
       s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8
+  // the 256-thread tiles of a request at most 2 in 5 of whose store's keys it
+  // asks for stage windows of 4 tiles (32 KiB: 4 blocks per CU instead of 8)
+  // — every 3rd key of the store: Push+Pull 333 -> 361 GB/s, every 4th 266 ->
+  // 276; every 2nd keeps 2 tiles (512 against 465 with 4;
+  // profiles/r4_ab_sparse_window.txt)
+  const bool wide = nt == 256 && 2 * s->size >= 5 * n;
   if (nt == 1024)
     k_resolve_apply<DT, OP, 1024><<<g, 1024, 0, st>>>(PSG_RA_ARGS);
+  else if (nt == 256 && (vec & 4) && (OP & PSG_PUSH) && sizeof(T) == 4 && wide)
+    k_resolve_apply<DT, OP, 256, true, 4><<<g, 256, 0, st>>>(PSG_RA_ARGS);
   else if (nt == 256 && (vec & 4) && (OP & PSG_PUSH) && sizeof(T) == 4)
     k_resolve_apply<DT, OP, 256, true><<<g, 256, 0, st>>>(PSG_RA_ARGS);
+  else if (nt == 256 && wide)
+    k_resolve_apply<DT, OP, 256, false, 4><<<g, 256, 0, st>>>(PSG_RA_ARGS);
   else if (nt == 512)
     k_resolve_apply<DT, OP, 512><<<g, 512, 0, st>>>(PSG_RA_ARGS);
   else
