@@ -240,7 +240,12 @@ int psg_store_handle(psg_store* s, int flags, const uint64_t* keys,
  * replies of the Pulls reaped so far are in memory (it synchronises their
  * stream once, rather than each request waiting for its own).  Every other
  * store call
- * completes the requests in flight first. */
+ * completes the requests in flight first.
+ * It can block: the first request of a key list sent as an identity request
+ * after K's generation changed (any insert, a clear) is a trial, reaped —
+ * with any replay it needs — before the call returns, so no request is
+ * launched behind a verdict not yet known; growing a key list's window cache
+ * also waits for the requests in flight. */
 int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys,
                            uint64_t first_key, const void* vals, void* out, uint64_t n,
                            psg_stream stream, uint64_t* ticket);

@@ -56,7 +56,6 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // the completed event promises what a stream synchronisation promises).
 // F_WINMISS: a cached window did not match its tile (searched inline).
 enum { F_MISSING = 0, F_WINMISS = 1, F_RANGE = 2, F_UNSORTED = 3, F_NFLAGS = 4 };
-// the host-memory completion word after the flags; never zeroed by reset_flags
 
 __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
   if (__ballot(cond) && (threadIdx.x & 63) == 0) flags[which] = 1;
@@ -187,27 +186,7 @@ __device__ __forceinline__ uint64_t lower_bound_dev(const uint64_t* __restrict__
 constexpr uint64_t kKeyPad = 2;
 constexpr int kWin = 2048;  // LDS-staged window of store keys (16 KiB: 10 blocks per CU)
 
-// lower_bound by one wave: 64 lanes probe 64 evenly spaced keys per round and
-// a ballot brackets the answer, so a 10 M-key store takes 4 rounds of one
-// parallel load instead of 24 dependent loads.  Wave-uniform result.
-__device__ __forceinline__ uint64_t lower_bound_wave(const uint64_t* __restrict__ a, uint64_t S,
-                                                     uint64_t key) {
-  const int lane = threadIdx.x & 63;
-  uint64_t lo = 0, hi = S;  // the answer is in [lo, hi]
-  while (hi - lo > 64) {
-    const uint64_t step = (hi - lo + 63) / 64;
-    const uint64_t p = lo + (uint64_t)lane * step;
-    const bool pred = p < hi && a[p] < key;
-    const uint64_t c = (uint64_t)__popcll(__ballot(pred));
-    if (c == 0) return lo;
-    const uint64_t pc = lo + c * step;
-    lo = lo + (c - 1) * step + 1;
-    hi = pc < hi ? pc : hi;
-  }
-  const uint64_t p = lo + (uint64_t)lane;
-  const bool pred = p < hi && a[p] < key;
-  return lo + (uint64_t)__popcll(__ballot(pred));
-}
+// lower_bound_wave: psg_internal.h
 
 // Pass 1: the store-key window of every 1024-key request tile, one wave per
 // tile: wlo[t] = lower_bound(K, q[t * kTile]); wlo[ntiles] = lower_bound(K, q[n-1]) + 1.
@@ -1271,12 +1250,12 @@ static int run_fixup(psg_store* s, int op, const void* vals, void* out, uint64_t
 // the error).  PSG_SYNC_POLL=0 always takes hipStreamSynchronize (A/B).
 //
 // Round 3 polled a word the stream wrote into pinned memory instead
-// (hipStreamWriteValue32).  Its documentation promises only that the write
+// (hipStreamWriteValue32), whose documentation promises only that the write
 // follows the earlier commands' execution, nothing about their writes being
-// visible to the next reader, and one LR Pull reply copied to the host right
-// after that word held an earlier reply's values over a tail of the buffer
-// (GPUTEST_r03, test_lr_ref_pin[3-200000-False-True-dyadic]).  Every hand-off
-// now rests on the documented event semantics.
+// visible to the next reader.  Every hand-off now rests on the documented
+// event semantics: a hardening step.  (GPUTEST_r03's red LR case was not a
+// hand-off: the reference LRServer installs its handle before InitWeight
+// runs, LRServer.h:70 vs 81-87 — DESIGN.md, "Parity".)
 static bool sync_poll() {
   static const bool on = [] {
     const char* e = getenv("PSG_SYNC_POLL");
@@ -2009,13 +1988,21 @@ static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
       // and of the requests behind it were never zeroed by a completing block
       // — a slot used again would start from a stale count — so every set is
       // zeroed (and the gate word cleared) once the device is idle.
+      // Only the streams of this store's requests are waited for (other
+      // stores' and the application's work may run on): the failed request's
+      // and those still in flight behind it.
+      std::vector<hipStream_t> sts{r.stream};
+      for (const InflightReq& g : s->inflight)
+        if (std::find(sts.begin(), sts.end(), g.stream) == sts.end()) sts.push_back(g.stream);
       s->inflight.clear();
       for (auto& c : s->wc) c.ident_trial = 0;
-      if (hipDeviceSynchronize() == hipSuccess) {
+      bool idle = true;
+      for (hipStream_t u : sts) idle = idle && hipStreamSynchronize(u) == hipSuccess;
+      if (idle) {
         constexpr size_t kCtrBytes = (size_t)kRing * (kArriveShards + 1) * kArriveStride * sizeof(uint64_t);
-        (void)hipMemset(s->done_ctr, 0, kCtrBytes);
-        (void)hipMemset(s->reject_dev + kPending, 0, sizeof(int));
-        (void)hipDeviceSynchronize();
+        (void)hipMemsetAsync(s->done_ctr, 0, kCtrBytes, r.stream);
+        (void)hipMemsetAsync(s->reject_dev + kPending, 0, sizeof(int), r.stream);
+        (void)hipStreamSynchronize(r.stream);
       }
       return rc;
     }

@@ -215,9 +215,10 @@ void RuntimeCopy(void* dst, const void* src, size_t bytes, int kind) {
 // own pinned staging blocks (StageToDevice / StageToHost: a DMA into or out of
 // a pinned block, an event waited for, a host memcpy), not the HIP runtime's
 // pageable-memory path: what the host reads is then exactly what the DMA
-// wrote once its event completed.  (A reply copied to pageable memory by the
-// runtime's own path once held an earlier reply's bytes over a tail of the
-// buffer — GPUTEST_r03; its staging is not ours to reason about.)
+// wrote once its event completed.  (A hardening step: the runtime's pageable
+// staging is not ours to reason about.  GPUTEST_r03's stale LR reply, first
+// blamed on it, was the reference LRServer's own constructor race —
+// LRServer.h:70 vs 81-87, DESIGN.md "Parity".)
 void CopySync(void* dst, const void* src, size_t bytes, int kind) {
   if (!bytes) return;
   if (kind == 0 && bytes > 64) return StageToDevice(dst, src, bytes);

@@ -301,21 +301,40 @@ struct Ring {
 };
 
 // The reader's answer to a connection's ring (ReadLoop), read by the writer
-// before its first message (Connect): false — 'N', the socket closed, or no
-// answer in 10 s — leaves every byte on the socket.
+// before its first message (Connect): 1 — 'Y', the ring carries the bytes; 0 —
+// an explicit 'N' (the reader could not map it), every byte on the socket; -1
+// — the socket closed, failed or gave no answer in PS_RING_ACK_MS (default
+// 10 s).  Only 'N' may fall back to the socket: a reader that maps the ring
+// after the writer gave up would read only the ring and take the socket's
+// bytes for doorbells, so -1 fails the connection instead.
+// PS_RING_ACK_DELAY_MS delays the reader's answer (fault injection, tests).
 constexpr char kRingYes = 'Y', kRingNo = 'N';
-bool RingAccepted(int fd) {
+int RingAccepted(int fd) {
+  static const int limit_ms = [] {
+    const char* e = std::getenv("PS_RING_ACK_MS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 10000;
+  }();
   pollfd pfd{fd, POLLIN, 0};
-  for (int waited = 0; waited < 10000; waited += 100) {
+  for (int waited = 0; waited < limit_ms; waited += 100) {
     const int pr = ::poll(&pfd, 1, 100);
-    if (pr < 0 && errno != EINTR) return false;
+    if (pr < 0 && errno != EINTR) return -1;
     if (pr > 0) {
       char a = 0;
       const ssize_t r = ::recv(fd, &a, 1, 0);
-      return r == 1 && a == kRingYes;
+      if (r != 1) return -1;
+      return a == kRingYes ? 1 : a == kRingNo ? 0 : -1;
     }
   }
-  return false;
+  errno = ETIMEDOUT;
+  return -1;
+}
+int RingAckDelayMs() {
+  static const int v = [] {
+    const char* e = std::getenv("PS_RING_ACK_DELAY_MS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
 }
 
 bool RingEnabled() {
@@ -987,7 +1006,11 @@ std::shared_ptr<Conn> TcpVan::Connect(int id) {
   const uint32_t hello[2] = {kHello, (uint32_t)name.size()};
   if (!WriteAll(fd, hello, sizeof(hello)) || (name.size() && !WriteAll(fd, name.data(), name.size())))
     return failed("hello to");  // (c closes fd)
-  if (c->ring && !RingAccepted(fd)) c->ring.reset();  // the reader could not map it: the socket carries all
+  if (c->ring) {
+    const int acc = RingAccepted(fd);
+    if (acc < 0) return failed("ring answer from");  // no answer: fail, never guess (c closes fd)
+    if (acc == 0) c->ring.reset();  // the reader could not map it: the socket carries all
+  }
   std::lock_guard<std::mutex> lk(peers_mu_);
   auto ins = conns_.emplace(id, c);
   return ins.first->second;  // a racing connect to the same peer: keep one
@@ -1074,7 +1097,14 @@ int TcpVan::SendMsg(const Message& msg) {
     Dispatch(m);
     return (int)sizeof(Meta) + msg.meta.data_size;
   }
-  std::shared_ptr<Conn> c = Connect(to);
+  // a connection whose ring got no answer in time is closed (Connect): try a
+  // fresh one twice more before the message fails
+  std::shared_ptr<Conn> c;
+  for (int attempt = 0; attempt < 3 && !(c = Connect(to)); ++attempt) {
+    const std::string why = LastConnectError();
+    if (why.rfind("ring answer", 0) != 0) break;  // not a ring answer (a peer that left): no retry
+    LOG(WARNING) << "connection to node " << to << " failed: " << why;
+  }
   if (!c) return -1;
   Node dst;
   {
@@ -1152,6 +1182,7 @@ void TcpVan::ReadLoop(int fd) {
       // carries the bytes, 'N' the socket does (a ring this process cannot map
       // — another /dev/shm behind the same hostname, or no room in it)
       const char ack = ring ? kRingYes : kRingNo;
+      if (RingAckDelayMs() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(RingAckDelayMs()));
       if (!WriteAll(fd, &ack, 1)) return;
     }
   }
@@ -1401,33 +1432,71 @@ static std::atomic<int> g_dump_lock{0};
 static void DumpOwnStack(int) {
   while (g_dump_lock.exchange(1, std::memory_order_acquire)) {
   }
-  char msg[96];
-  const int n = std::snprintf(msg, sizeof(msg), "[node %d] thread %d:\n", (int)getpid(), (int)gettid());
-  if (n > 0) (void)!::write(2, msg, (size_t)n);
+  // "[thread <tid>]:" formatted by hand (no stdio in a handler)
+  char msg[40] = "[thread ";
+  int n = 8;
+  char digits[12];
+  int nd = 0;
+  for (long t = (long)::syscall(SYS_gettid); t > 0 && nd < 12; t /= 10) digits[nd++] = (char)('0' + t % 10);
+  while (nd > 0) msg[n++] = digits[--nd];
+  msg[n++] = ']';
+  msg[n++] = ':';
+  msg[n++] = '\n';
+  (void)!::write(2, msg, (size_t)n);
   void* frames[48];
   const int k = ::backtrace(frames, 48);
   ::backtrace_symbols_fd(frames, k, 2);
   g_dump_lock.store(0, std::memory_order_release);
 }
+// Lists the threads with raw open / getdents64 / close system calls (no
+// opendir / readdir: they allocate, and the interrupted thread may hold the
+// malloc lock), and parses each name by hand.
 static void DumpAllStacks(int) {
-  char msg[80];
-  const int n = std::snprintf(msg, sizeof(msg), "[node %d] SIGQUIT: stacks of every thread follow\n", (int)getpid());
-  if (n > 0) (void)!::write(2, msg, (size_t)n);
-  if (DIR* d = ::opendir("/proc/self/task")) {
-    while (dirent* e = ::readdir(d)) {
-      const int tid = std::atoi(e->d_name);
-      if (tid > 0) ::syscall(SYS_tgkill, (int)getpid(), tid, SIGUSR2);
+  static const char kHead[] = "[node] SIGQUIT: stacks of every thread follow\n";
+  (void)!::write(2, kHead, sizeof(kHead) - 1);
+  const int fd = (int)::syscall(SYS_open, "/proc/self/task", O_RDONLY | O_DIRECTORY);
+  if (fd < 0) return;
+  alignas(8) char buf[4096];
+  const int pid = (int)::syscall(SYS_getpid);
+  for (;;) {
+    const long got = ::syscall(SYS_getdents64, fd, buf, sizeof(buf));
+    if (got <= 0) break;
+    for (long off = 0; off < got;) {
+      // struct linux_dirent64: ino 8, off 8, reclen 2, type 1, name
+      unsigned short reclen;
+      std::memcpy(&reclen, buf + off + 16, sizeof(reclen));
+      const char* name = buf + off + 19;
+      int tid = 0;
+      bool digits = *name != '\0';
+      for (const char* c = name; *c; ++c) {
+        if (*c < '0' || *c > '9') {
+          digits = false;
+          break;
+        }
+        tid = tid * 10 + (*c - '0');
+      }
+      if (digits && tid > 0) ::syscall(SYS_tgkill, pid, tid, SIGUSR2);
+      off += reclen;
     }
-    ::closedir(d);
   }
+  ::syscall(SYS_close, fd);
 }
 
 int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** argv) {
   const char* role = RoleOf(argc, argv);
   CHECK(role) << "process mode needs a role (argv[3] or PS_ROLE)";
   for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL}) ::signal(sig, FatalSignal);
-  ::signal(SIGUSR2, DumpOwnStack);
-  ::signal(SIGQUIT, DumpAllStacks);
+  // the stack dump only when the job has a deadline (the launcher's
+  // PS_JOB_TIMEOUT_S) or PS_STACK_DUMP=1 asks for it: otherwise a drop-in
+  // application's own SIGQUIT / SIGUSR2 handlers stay as it set them
+  const char* jt = std::getenv("PS_JOB_TIMEOUT_S");
+  const char* sd = std::getenv("PS_STACK_DUMP");
+  if ((jt && std::atoi(jt) > 0) || (sd && std::atoi(sd) != 0)) {
+    void* warm[2];
+    (void)::backtrace(warm, 2);  // loads libgcc's unwinder now, not inside a handler
+    ::signal(SIGUSR2, DumpOwnStack);
+    ::signal(SIGQUIT, DumpAllStacks);
+  }
   ReadLocalConfigToEnv(argv[1]);
   shm::Enable();
   const int ns = Environment::GetIntOrDefault("PS_NUM_SERVER", 1);
@@ -1546,6 +1615,7 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
   // the stacks of all its threads (SIGQUIT, DumpAllStacks), then all are killed
   int rc = 0;
   size_t left = pids.size();
+  std::vector<char> reaped(pids.size(), 0);  // waitpid has returned it: never signal that pid again
   auto failed_at = std::chrono::steady_clock::time_point::max();
   const int job_timeout_s = Environment::GetIntOrDefault("PS_JOB_TIMEOUT_S", 0);
   auto job_deadline = job_timeout_s > 0 ? std::chrono::steady_clock::now() + std::chrono::seconds(job_timeout_s)
@@ -1554,11 +1624,13 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
     if (std::chrono::steady_clock::now() > job_deadline) {
       std::fprintf(stderr, "[launcher] job still running after PS_JOB_TIMEOUT_S=%d s: stacks of every node follow\n",
                    job_timeout_s);
-      for (pid_t q : pids) {  // one node at a time: their dumps share stderr
-        kill(q, SIGQUIT);
+      for (size_t k = 0; k < pids.size(); ++k) {  // one node at a time: their dumps share stderr
+        if (reaped[k]) continue;  // (its pid may belong to another process by now)
+        kill(pids[k], SIGQUIT);
         std::this_thread::sleep_for(std::chrono::milliseconds(500));
       }
-      for (pid_t q : pids) kill(q, SIGKILL);
+      for (size_t k = 0; k < pids.size(); ++k)
+        if (!reaped[k]) kill(pids[k], SIGKILL);
       rc = 124;
       failed_at = std::chrono::steady_clock::time_point::max();
       job_deadline = std::chrono::steady_clock::time_point::max();
@@ -1568,9 +1640,10 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
     if (p > 0) {
       --left;
       const bool bad = !WIFEXITED(status) || WEXITSTATUS(status) != 0;
+      size_t k = 0;
+      while (k < pids.size() && pids[k] != p) ++k;
+      if (k < reaped.size()) reaped[k] = 1;
       if (WIFSIGNALED(status)) {
-        size_t k = 0;
-        while (k < pids.size() && pids[k] != p) ++k;
         std::fprintf(stderr, "[launcher] node process %d (%s) killed by signal %d\n", (int)p,
                      k < logs.size() ? logs[k].c_str() : "?", WTERMSIG(status));
       }
@@ -1582,7 +1655,8 @@ int Launch(int num_servers, int num_workers, int argc, char** argv) {
     }
     if (p < 0 && errno != EINTR) break;
     if (rc && std::chrono::steady_clock::now() - failed_at > std::chrono::seconds(30)) {
-      for (pid_t q : pids) kill(q, SIGKILL);
+      for (size_t k = 0; k < pids.size(); ++k)
+        if (!reaped[k]) kill(pids[k], SIGKILL);
       failed_at = std::chrono::steady_clock::time_point::max();
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(5));

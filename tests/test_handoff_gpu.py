@@ -1,12 +1,12 @@
 """A Pull reply handed out by the store's completion wait holds the request's
 values (tests/harness/unit/handoff_stress.cpp).
 
-GPUTEST_r03 caught the LR handle answering a Pull with an earlier reply's
-values over a tail of the buffer (ps/lr_handle.h; the reference answers with
-the post-update weights, tests/src/LRServer.h:163-177, 196-206).  The waits a
-server makes before answering now rest on events (psg_store.hip,
+The waits a server makes before answering rest on events (psg_store.hip,
 stream_done / wait_landed) and the host copies on this runtime's own pinned
-staging (src/device.cc).  Each case below runs the exact answer sequence many
+staging (src/device.cc): a hardening step taken while GPUTEST_r03's red LR
+case was open.  That case was the reference LRServer's own constructor race
+(its handle installed before InitWeight, tests/src/LRServer.h:70 vs 81-87;
+DESIGN.md "Parity"), not a hand-off.  Each case below runs the exact answer sequence many
 times — update, Pull into one reply buffer, wait, copy out on the same stream —
 and checks every element of every reply; with several threads, as in the
 thread-mode cluster, each on its own stream.
