@@ -192,7 +192,11 @@ int psg_store_clear(psg_store* s, psg_stream stream);
 #define PSG_CTR_IDENT 1
 #define PSG_CTR_NOTIDENT 2
 #define PSG_CTR_ORDERED 3
-#define PSG_NCOUNTERS 4
+/* runs of queued Pushes served in one pass (psg_store_push_frames,
+ * psg_store_push_slots_frames), and the requests those runs held */
+#define PSG_CTR_RUNS 4
+#define PSG_CTR_RUN_FRAMES 5
+#define PSG_NCOUNTERS 6
 int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):
@@ -251,6 +255,32 @@ int psg_store_handle_async(psg_store* s, int flags, const uint64_t* keys,
                            psg_stream stream, uint64_t* ticket);
 int psg_store_wait(psg_store* s, uint64_t ticket);
 
+/* A run of k Push requests on ONE key list, queued one behind the other at a
+ * server (the reference's KVServer drains its queue one message at a time,
+ * src/internal/Customer.cpp:52-70, and applies each with `store[key] +=
+ * vals[i]`, src/ps/KVApp.h:446-454).  The result is bit for bit that of
+ *     for j < k:  psg_store_handle(s, PSG_PUSH, keys_host[j], first_key,
+ *                                  vals_host[j], NULL, n, stream)
+ * — each key's frames added in order j = 0, 1, ..., every add rounded to the
+ * store's dtype as k requests round — but when the lists are one list, the
+ * store is read and written once for the k frames: 8 + 4k B per f32 key
+ * instead of 12k, plus reading each list once to know that it is the same
+ * (8 B per list).  keys_host: k device key arrays of n keys (pointers may
+ * differ: each worker's own frame), or NULL for a dense run on a DENSE store
+ * (consecutive keys from first_key).  vals_host: k device value arrays.
+ * 1 <= k <= 16.  On a SORTED store one pass serves lists that are a stretch
+ * of the store's keys, or, failing that, lists equal to list 0 whose keys are
+ * all present, in range and ascending; any other run — lists that differ,
+ * absent keys, keys out of order — is served request by request, exactly as
+ * k psg_store_handle calls (a request that fails stops the run there and
+ * returns its status).  *fused_host (may be NULL) = 1 when one pass served the
+ * run.  Returns as psg_store_handle does: the frames are no longer read (a
+ * dense run on a DENSE store: stream-ordered, like a dense request).
+ * PSG_FRAMES=0 serves every run request by request (A/B). */
+int psg_store_push_frames(psg_store* s, const uint64_t* const* keys_host, uint64_t first_key,
+                          const void* const* vals_host, int k, uint64_t n, psg_stream stream,
+                          int* fused_host);
+
 /* The stable device radix sort of the order-preserving path (psg_sort.hip),
  * exported for its parity tests: sorts (keys[i], vals[i]) by bits [0, bits) of
  * the key, equal keys keeping their order.  In place; synchronises `stream`
@@ -281,6 +311,14 @@ int psg_store_slots_stretch(psg_store* s, const uint32_t* slots, uint64_t n, uin
                             psg_stream stream);
 int psg_store_handle_stretch(psg_store* s, int flags, uint64_t first, const void* vals, void* out,
                              uint64_t n, psg_stream stream);
+/* A run of k Pushes on one cached list (LR key caching names it by its hash,
+ * tests/src/LRServer.h:127-142): psg_store_handle_slots(PSG_PUSH) with
+ * vals_host[0], then vals_host[1], ... in one pass — slot 4 + store 8 + 4k B
+ * per f32 key; slots == NULL: psg_store_handle_stretch on [first, first + n),
+ * 8 + 4k.  Bit for bit the k requests in order.  Stream-ordered, like them
+ * (psg_store_sync before answering).  1 <= k <= 16. */
+int psg_store_push_slots_frames(psg_store* s, const uint32_t* slots, uint64_t first,
+                                const void* const* vals_host, int k, uint64_t n, psg_stream stream);
 /* Return once everything enqueued on `stream` so far has run, its writes
  * visible to any agent (a slot or stretch request's values no longer read, its
  * Pull reply in memory for a copy engine, the host or another process): an

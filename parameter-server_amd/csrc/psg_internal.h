@@ -282,6 +282,23 @@ int dense_request(int dtype, int op, void* store_vals, const void* vals, void* o
 // Slot-indexed request (gather/scatter).  psg_dense.hip.
 int slot_request(int dtype, int op, void* store_vals, const uint32_t* slots,
                  const void* vals, void* out, uint64_t n, hipStream_t stream);
+// A run of queued Pushes on one key list applied in one pass (psg_frames.hip).
+// frames_base: *base = D, the slot of q0[0] in K[0..S) when K[D .. D + n) can
+//   hold the list, else UINT64_MAX (one wave);
+// frames_check: lists keys[j0..k) equal ref[*base + i] (base NULL: ref[i]) for
+//   i < n, else *rej = seq;
+// frames_apply: store[*base + i] (base NULL: store[i]) += vals[0][i], then
+//   vals[1][i], ... in order — unless *base is UINT64_MAX or *rej == seq, when
+//   it writes nothing and sets *flag (pinned host int);
+// frames_slots: the same on store[slots[i]] (slots unique).
+constexpr int kMaxFrames = 16;
+int frames_base(const uint64_t* K, uint64_t S, const uint64_t* q0, uint64_t n, uint64_t* base, hipStream_t st);
+int frames_check(const uint64_t* ref, const uint64_t* base, const uint64_t* const* keys, int j0, int k, uint64_t n,
+                 int* rej, int seq, hipStream_t st);
+int frames_apply(int dtype, void* store_vals, uint64_t store_elems, const void* const* vals, int k, uint64_t n,
+                 const uint64_t* base, const int* rej, int seq, int* flag, hipStream_t st);
+int frames_slots(int dtype, void* store_vals, const uint32_t* slots, const void* const* vals, int k, uint64_t n,
+                 const int* rej, int seq, int* flag, hipStream_t st);
 // Stable LSD radix sort on bits [0, bits) of keys[n], carrying u32 values
 // (iota: the values are the positions 0..n-1 and vals is not read).  Ping-pongs
 // between (keys, vals) and (keys_alt, vals_alt); *result = 0 or 1 names the

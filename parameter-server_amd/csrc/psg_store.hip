@@ -73,6 +73,9 @@ enum { W_MISSING = 1, W_WINMISS = 2, W_RANGE = 4, W_UNSORTED = 8, W_GATED = 16, 
 // reports W_GATED, and the host replays it after that follow-up.
 // [kRejIdent]: an identity request's check (k_ident_check) failed.
 constexpr int kRejRange = 0, kRejUnsorted = 1, kPending = 2, kRejIdent = 3;
+// [kFramesBase, +2): a uint64 — the stretch base of a run of Pushes
+// (psg_store_push_frames, frames_base), read by its check and apply kernels.
+constexpr int kFramesBase = 8;
 
 // The store-key window of one request tile: [lo, hi) of K brackets every key
 // between the tile's first and last key (lo = lower_bound(K, first), hi =
@@ -2182,6 +2185,75 @@ static int handle_sync(psg_store* s, int flags, const uint64_t* keys, uint64_t f
   return own_rc;
 }
 
+// ---- a run of queued Pushes on one key list (psg_frames.hip) --------------
+// PSG_FRAMES=0: every run is served request by request (A/B).
+static bool frames_on() {
+  static const bool on = [] {
+    const char* e = getenv("PSG_FRAMES");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// The k requests one after the other, each to completion: the reference's
+// sequence, and the fallback of every run the one-pass forms do not cover.
+static int frames_one_by_one(psg_store* s, const uint64_t* const* keys, uint64_t first_key,
+                             const void* const* vals, int k, uint64_t n, hipStream_t st) {
+  for (int j = 0; j < k; ++j)
+    PSG_TRY(handle_sync(s, PSG_PUSH, keys ? keys[j] : nullptr, first_key, vals[j], nullptr, n, st));
+  return PSG_OK;
+}
+
+static void count_run(psg_store* s, int k) {
+  s->counters[PSG_CTR_RUNS]++;
+  s->counters[PSG_CTR_RUN_FRAMES] += (uint64_t)k;
+}
+
+// Runs on a SORTED store: (1) the lists are a stretch K[D, D + n) of the
+// store — frames_base, frames_check of every list against it, frames_apply,
+// one flag read; (2) else list 0 resolved to slots (no key absent, in range,
+// ascending), lists 1..k-1 checked against list 0, frames_slots; (3) else one
+// by one.  A failed check wrote nothing (the apply kernels read its word
+// first), so every fallback starts from the store the run found.
+static int frames_sorted(psg_store* s, const uint64_t* const* keys, const void* const* vals, int k, uint64_t n,
+                         hipStream_t st, int* fused) {
+  if (!sorted_fused() || s->size == 0 || n > s->size) return frames_one_by_one(s, keys, 0, vals, k, n, st);
+  uint64_t* base = reinterpret_cast<uint64_t*>(s->reject_dev + kFramesBase);
+  int* rej = s->reject_dev + kRejIdent;
+  int seq = next_seq(s);
+  reset_flags(s);
+  PSG_TRY(frames_base(s->keys, s->size, keys[0], n, base, st));
+  PSG_TRY(frames_check(s->keys, base, keys, 0, k, n, rej, seq, st));
+  PSG_TRY(frames_apply(s->dtype, s->vals, s->size, vals, k, n, base, rej, seq, s->flags + F_MISSING, st));
+  PSG_TRY(read_flags(s, st));
+  if (!s->flags_host[F_MISSING]) {
+    *fused = 1;
+    count_run(s, k);
+    return PSG_OK;
+  }
+  PSG_TRY(ensure_slots(s, n));
+  PSG_TRY(launch_resolve(s, keys[0], n, s->slots, st));
+  PSG_TRY(read_flags(s, st));
+  const int* f = s->flags_host;
+  if (f[F_MISSING] || f[F_RANGE] || f[F_UNSORTED]) return frames_one_by_one(s, keys, 0, vals, k, n, st);
+  seq = next_seq(s);
+  reset_flags(s);
+  PSG_TRY(frames_check(keys[0], nullptr, keys, 1, k, n, rej, seq, st));
+  PSG_TRY(frames_slots(s->dtype, s->vals, s->slots, vals, k, n, rej, seq, s->flags + F_MISSING, st));
+  PSG_TRY(read_flags(s, st));
+  if (s->flags_host[F_MISSING]) return frames_one_by_one(s, keys, 0, vals, k, n, st);
+  *fused = 1;
+  count_run(s, k);
+  return PSG_OK;
+}
+
+static int frames_args(psg_store* s, const void* const* vals_host, int k) {
+  PSG_REQUIRE(s && vals_host, PSG_ERR_INVALID, "push frames: null argument");
+  PSG_REQUIRE(k >= 1 && k <= kMaxFrames, PSG_ERR_INVALID, "push frames: 1..%d frames, got %d", kMaxFrames, k);
+  for (int j = 0; j < k; ++j) PSG_REQUIRE(vals_host[j], PSG_ERR_INVALID, "push frames: null vals of frame %d", j);
+  return PSG_OK;
+}
+
 }  // namespace psg
 
 using namespace psg;
@@ -2466,6 +2538,64 @@ int psg_store_handle_slots(psg_store* s, int flags, const uint32_t* slots, const
   PSG_REQUIRE(!(flags & PSG_PULL) || out, PSG_ERR_INVALID, "pull without out buffer");
   PSG_TRY(drain(s));
   return slot_request(s->dtype, flags, s->vals, slots, vals, out, n, (hipStream_t)stream);
+}
+
+int psg_store_push_frames(psg_store* s, const uint64_t* const* keys_host, uint64_t first_key,
+                          const void* const* vals_host, int k, uint64_t n, psg_stream stream, int* fused_host) {
+  if (fused_host) *fused_host = 0;
+  PSG_TRY(frames_args(s, vals_host, k));
+  if (keys_host)
+    for (int j = 0; j < k; ++j) PSG_REQUIRE(keys_host[j], PSG_ERR_INVALID, "push frames: null keys of frame %d", j);
+  if (n == 0) return PSG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  PSG_TRY(drain(s));
+  if (k == 1 || !frames_on()) return frames_one_by_one(s, keys_host, first_key, vals_host, k, n, st);
+  int fused = 0;
+  if (s->kind == PSG_STORE_DENSE) {
+    if (keys_host) return frames_one_by_one(s, keys_host, first_key, vals_host, k, n, st);
+    PSG_REQUIRE(first_key >= s->key_begin && first_key - s->key_begin <= s->capacity &&
+                    n <= s->capacity - (first_key - s->key_begin),
+                PSG_ERR_RANGE, "dense run [%llu, +%llu) outside store slots [%llu, +%llu)",
+                (unsigned long long)first_key, (unsigned long long)n, (unsigned long long)s->key_begin,
+                (unsigned long long)s->capacity);
+    char* at = (char*)s->vals + (first_key - s->key_begin) * s->esize;
+    PSG_TRY(frames_apply(s->dtype, at, s->capacity, vals_host, k, n, nullptr, nullptr, 0, s->flags + F_MISSING, st));
+    fused = 1;
+    count_run(s, k);
+  } else {
+    PSG_REQUIRE(keys_host, PSG_ERR_INVALID, "SORTED store needs explicit keys");
+    PSG_TRY(frames_sorted(s, keys_host, vals_host, k, n, st, &fused));
+  }
+  if (fused_host) *fused_host = fused;
+  return PSG_OK;
+}
+
+int psg_store_push_slots_frames(psg_store* s, const uint32_t* slots, uint64_t first, const void* const* vals_host,
+                                int k, uint64_t n, psg_stream stream) {
+  PSG_TRY(frames_args(s, vals_host, k));
+  if (n == 0) return PSG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  PSG_TRY(drain(s));
+  if (!slots) {
+    const uint64_t limit = s->kind == PSG_STORE_SORTED ? s->size : s->capacity;
+    PSG_REQUIRE(first <= limit && n <= limit - first, PSG_ERR_RANGE,
+                "push frames: slots [%llu, %llu) past the store's %llu", (unsigned long long)first,
+                (unsigned long long)(first + n), (unsigned long long)limit);
+    char* at = (char*)s->vals + first * (uint64_t)s->esize;
+    if (k == 1 || !frames_on()) {
+      for (int j = 0; j < k; ++j) PSG_TRY(dense_request(s->dtype, PSG_PUSH, at, vals_host[j], nullptr, n, st));
+      return PSG_OK;
+    }
+    PSG_TRY(frames_apply(s->dtype, at, limit, vals_host, k, n, nullptr, nullptr, 0, s->flags + F_MISSING, st));
+  } else {
+    if (k == 1 || !frames_on()) {
+      for (int j = 0; j < k; ++j) PSG_TRY(slot_request(s->dtype, PSG_PUSH, s->vals, slots, vals_host[j], nullptr, n, st));
+      return PSG_OK;
+    }
+    PSG_TRY(frames_slots(s->dtype, s->vals, slots, vals_host, k, n, nullptr, 0, s->flags + F_MISSING, st));
+  }
+  count_run(s, k);
+  return PSG_OK;
 }
 
 int psg_store_dump(psg_store* s, uint64_t* keys_host, void* vals_host) {

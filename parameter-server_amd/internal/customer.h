@@ -56,6 +56,18 @@ class ThreadsafePQueue {
     }
     cv_.notify_one();
   }
+  /* the message WaitAndPop would return next, popped only when take(it) says
+   * so; never waits (a server draining a run of queued Pushes) */
+  template <typename Pred>
+  bool PopIf(Pred take, Message* out) {
+    if (size_.load(std::memory_order_acquire) == 0) return false;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (queue_.empty() || !take(queue_.top())) return false;
+    *out = queue_.top();
+    queue_.pop();
+    size_.store(queue_.size(), std::memory_order_release);
+    return true;
+  }
   Message WaitAndPop() {
     SpinFor([this] { return size_.load(std::memory_order_acquire) > 0; });
     std::unique_lock<std::mutex> lk(mu_);
@@ -97,6 +109,13 @@ class Customer {
   void AddResponse(int request_id, int cnt = 1);
   /* called by the Van for every data message to this customer */
   void OnReceive(const Message& received) { receive_queue_.Push(received); }
+  /* From the receive thread's handle: take the next queued message if take(it)
+   * — exactly the one the thread would handle next, so the order of handling
+   * is unchanged (a KVServer serving a run of queued Pushes in one pass). */
+  template <typename Pred>
+  bool TakeQueued(Pred take, Message* out) {
+    return receive_queue_.PopIf(take, out);
+  }
 
   int app_id() const { return app_id_; }
   int customer_id() const { return customer_id_; }

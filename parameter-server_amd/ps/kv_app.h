@@ -18,8 +18,12 @@
 // (HBM frames are copied to host first), exactly like the reference; a handle
 // that can consume HBM frames registers with SetDeviceRequestHandle.
 #pragma once
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -125,6 +129,32 @@ inline uint64_t KeyListHash(const Key* keys, size_t n) {
     seed ^= x ^ x >> 31;
   }
   return seed;
+}
+
+/* PS_PUSH_RUNS=0: a server handles every queued Push on its own, never a run
+ * of them in one pass (A/B; KVServer::OnReceive). */
+inline bool PushRunsOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_PUSH_RUNS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+/* PS_TRACE_REQUESTS=<file>: every request a KVServer hands to its handle is
+ * appended to <file> as one line "server sender timestamp push pull keys
+ * run_size run_pos" (run_size 1 for a request handled on its own) — the
+ * arrival order a test replays through the oracle.  One write(2) per line on
+ * an O_APPEND descriptor, so the servers of a job may share the file. */
+inline void TraceRequest(int server, const KVMeta& m, size_t keys, size_t run_size, size_t run_pos) {
+  static const int fd = [] {
+    const char* e = std::getenv("PS_TRACE_REQUESTS");
+    return e && *e ? ::open(e, O_WRONLY | O_CREAT | O_APPEND, 0644) : -1;
+  }();
+  if (fd < 0) return;
+  char line[160];
+  const int len = std::snprintf(line, sizeof(line), "%d %d %d %d %d %zu %zu %zu\n", server, m.sender, m.timestamp,
+                                (int)m.push, (int)m.pull, keys, run_size, run_pos);
+  if (len > 0) (void)!::write(fd, line, (size_t)len);
 }
 
 /* ZPull offers the servers its HBM output (Meta::direct_reply); PS_DIRECT_REPLY=0
@@ -303,6 +333,11 @@ template <typename Value>
 class KVServer : public SimpleApp {
  public:
   using ReqHandle = std::function<void(const KVMeta& req_meta, const KVPairs<Value>& req_data, KVServer* server)>;
+  /* A run of Pushes queued one behind the other (see OnReceive), in arrival
+   * order; the handle answers every one of them. */
+  using RunHandle = std::function<void(const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& data,
+                                       KVServer* server)>;
+  static constexpr int kMaxRun = 16;  // requests a run holds at most (psg_store_push_frames)
 
   explicit KVServer(int app_id) : SimpleApp() {
     app_id_ = app_id;
@@ -318,8 +353,12 @@ class KVServer : public SimpleApp {
     CHECK(static_cast<bool>(request_handle)) << "invalid request handle";
     Install(request_handle, false);
   }
-  /* the default handle keeps its store in HBM and takes frames where they are */
-  void SetRequestHandle(const KVServerDefaultHandle<Value>& h) { Install(h, true); }
+  /* the default handle keeps its store in HBM and takes frames where they are,
+   * and serves a run of queued Pushes on one key list in one pass */
+  void SetRequestHandle(const KVServerDefaultHandle<Value>& h) {
+    Install(h, true, [hd = h](const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& data,
+                         KVServer* server) mutable { hd.PushRun(metas, data, server); });
+  }
   /* a handle that consumes HBM frames itself */
   void SetDeviceRequestHandle(const ReqHandle& request_handle) {
     CHECK(static_cast<bool>(request_handle)) << "invalid request handle";
@@ -331,14 +370,26 @@ class KVServer : public SimpleApp {
 
  private:
   void OnReceive(const Message& msg) override;
-  void Install(const ReqHandle& h, bool device_frames) {
+  void Install(const ReqHandle& h, bool device_frames, const RunHandle& run = nullptr) {
     {
       std::lock_guard<std::mutex> lk(handle_mu_);
       request_handle_ = h;
+      run_handle_ = run;
       device_frames_ = device_frames;
     }
     handle_cv_.notify_all();
   }
+  static KVMeta MetaOf(const Message& msg) {
+    KVMeta meta;
+    meta.cmd = msg.meta.head;
+    meta.push = msg.meta.push;
+    meta.pull = msg.meta.pull;
+    meta.sender = msg.meta.sender;
+    meta.timestamp = msg.meta.timestamp;
+    meta.customer_id = msg.meta.customer_id;
+    return meta;
+  }
+  RunHandle run_handle_;
   // The customer thread may receive a request before the program installs its
   // handle (it is created with the KVServer); it waits for the handle instead
   // of failing the reference's CHECK (KVApp.h:487) on that race.
@@ -463,6 +514,78 @@ struct KVServerDefaultHandle {
     server->Response(req_meta, res);
   }
 
+  /* A run of Pushes queued one behind the other (KVServer::OnReceive), with the
+   * result of handling them one at a time in that order (KVApp.h:446-454 per
+   * request).  Full key lists go to psg_store_push_frames, which reads and
+   * writes the store once for the whole run when the lists are one list, and
+   * serves them request by request otherwise.  With the key cache, a run of
+   * requests naming one cached list by its hash is one pass over the cached
+   * slots or stretch (psg_store_push_slots_frames).  Every request is answered
+   * after the run is applied. */
+  void PushRun(const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& datas, KVServer<Value>* server) {
+    const int dev = PostOffice::Get()->device();
+    CHECK_GE(dev, 0) << "KVServerDefaultHandle: the value store lives in HBM and this node has no GPU";
+    constexpr int dt = device::DType<Value>();
+    CHECK_GE(dt, 0) << "KVServerDefaultHandle: value type not supported by the HBM store";
+    if (!state->store)
+      device::Check(psg_store_create(PSG_STORE_SORTED, dt, 0, kMaxKey, 0, &state->store), "psg_store_create");
+    psg_stream s = device::ThreadStream();
+    const size_t k = datas.size();
+    const size_t n = datas[0].keys.size();
+    for (const auto& d : datas) {
+      CHECK_EQ(d.keys.size(), n);
+      CHECK_EQ(n, d.vals.size());
+    }
+    std::vector<SVector<Value>> dvals(k);
+    std::vector<const void*> vp(k);
+    if (state->key_cache && n == 1) {
+      // cached lists named by their hashes (LRServer.h:129-135); consecutive
+      // requests naming one list are one pass
+      std::vector<Key> h(k);
+      for (size_t j = 0; j < k; ++j) {
+        if (datas[j].keys.on_device()) device::CopySync(&h[j], datas[j].keys.data(), sizeof(Key), 1);
+        else h[j] = datas[j].keys[0];
+      }
+      for (size_t i = 0; i < k;) {
+        size_t e = i + 1;
+        while (e < k && h[e] == h[i]) ++e;
+        auto it = state->cache.find(h[i]);
+        CHECK(it != state->cache.end()) << "Keys don't exist with hash value: " << h[i];
+        Cached& c = it->second;
+        Refresh(c, s);
+        for (size_t j = i; j < e; ++j) {
+          CHECK_EQ(c.keys.size(), datas[j].vals.size());
+          dvals[j] = detail::ToDeviceAsync(datas[j].vals, dev);
+          vp[j] = dvals[j].data();
+        }
+        const bool stretch = c.stretch != UINT64_MAX;
+        device::Check(psg_store_push_slots_frames(state->store, stretch ? nullptr : c.slots.data(),
+                                                  stretch ? c.stretch : 0, vp.data() + i, (int)(e - i),
+                                                  c.keys.size(), s),
+                      "psg_store_push_slots_frames");
+        i = e;
+      }
+      device::Check(psg_store_sync(state->store, s), "psg_store_sync");
+    } else {
+      std::vector<SVector<Key>> dkeys(k);
+      std::vector<const uint64_t*> kp(k);
+      for (size_t j = 0; j < k; ++j) {
+        dkeys[j] = detail::ToDeviceAsync(datas[j].keys, dev);
+        dvals[j] = detail::ToDeviceAsync(datas[j].vals, dev);
+        kp[j] = dkeys[j].data();
+        vp[j] = dvals[j].data();
+      }
+      int fused = 0;
+      device::Check(psg_store_push_frames(state->store, kp.data(), 0, vp.data(), (int)k, n, s, &fused),
+                    "psg_store_push_frames");
+      if (state->key_cache)
+        for (size_t j = 0; j < k; ++j)
+          Remember(dkeys[j], datas[j].keys.on_device(),
+                   datas[j].keys.on_device() ? 0 : detail::KeyListHash(datas[j].keys.data(), n), s);
+    }
+    for (const KVMeta& m : metas) server->Response(m, KVPairs<Value>());
+  }
+
   psg_store* store() const { return state->store; }
   size_t cached_key_lists() const { return state->cache.size(); }
   /* (key, value) pairs in key order, copied to host */
@@ -537,19 +660,15 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     SimpleApp::OnReceive(msg);
     return;
   }
-  KVMeta meta;
-  meta.cmd = msg.meta.head;
-  meta.push = msg.meta.push;
-  meta.pull = msg.meta.pull;
-  meta.sender = msg.meta.sender;
-  meta.timestamp = msg.meta.timestamp;
-  meta.customer_id = msg.meta.customer_id;
+  const KVMeta meta = MetaOf(msg);
   bool device_frames, installed;
+  RunHandle run;
   {
     std::unique_lock<std::mutex> lk(handle_mu_);
     handle_cv_.wait_for(lk, std::chrono::seconds(30), [this] { return static_cast<bool>(request_handle_); });
     installed = static_cast<bool>(request_handle_);
     device_frames = device_frames_;
+    run = run_handle_;
   }
   CHECK(installed) << "no request handle installed 30 s after the first request";
   KVPairs<Value> data;
@@ -585,6 +704,40 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       data.lens = detail::ToHost(data.lens);
     }
   }
+  // A run of Pushes.  The reference's receive thread handles the queued
+  // messages one at a time, in queue order (Customer.cpp:52-70); a plain Push
+  // taken here may bring along the Pushes queued right behind it — the very
+  // messages the thread would handle next, so nothing is reordered — when they
+  // have the same shape (push only, as many keys and values, no lens, no reply
+  // offer).  The run's handle (KVServerDefaultHandle::PushRun) serves them as
+  // that sequence: one pass when their key lists are one list (nw workers of
+  // a BSP round), request by request otherwise.
+  if (run && device_frames && detail::PushRunsOn() && meta.push && !meta.pull && !msg.meta.direct_reply && n == 2 &&
+      data.keys.size()) {
+    const size_t kbytes = msg.data[0].size(), vbytes = msg.data[1].size();
+    auto mate = [&](const Message& m) {
+      return m.meta.request && !m.meta.simple_app && m.meta.control.cmd == Control::EMPTY && m.meta.push &&
+             !m.meta.pull && !m.meta.direct_reply && m.meta.app_id == msg.meta.app_id && m.data.size() == 2 &&
+             m.data[0].size() == kbytes && m.data[1].size() == vbytes;
+    };
+    std::vector<KVMeta> metas{meta};
+    std::vector<KVPairs<Value>> datas{data};
+    Message next;
+    while ((int)metas.size() < kMaxRun && customer_->TakeQueued(mate, &next)) {
+      metas.push_back(MetaOf(next));
+      KVPairs<Value> d;
+      d.keys = next.data[0];
+      d.vals = next.data[1];
+      datas.push_back(std::move(d));
+    }
+    if (metas.size() > 1) {
+      for (size_t j = 0; j < metas.size(); ++j)
+        detail::TraceRequest(PostOffice::Get()->my_id(), metas[j], datas[j].keys.size(), metas.size(), j);
+      run(metas, datas, this);
+      return;
+    }
+  }
+  detail::TraceRequest(PostOffice::Get()->my_id(), meta, data.keys.size(), 1, 0);
   // called in place: a handle keeps its state across requests (KVApp.h:457)
   request_handle_(meta, data, this);
   direct_out_ = SVector<Value>();

@@ -43,7 +43,7 @@ EXPORTS = [
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear", "psg_store_counters",
     "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots",
     "psg_store_slots_stretch", "psg_store_handle_stretch", "psg_store_sync", "psg_store_dump",
-    "psg_key_list_hash",
+    "psg_key_list_hash", "psg_store_push_frames", "psg_store_push_slots_frames",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
@@ -125,6 +125,9 @@ def lib() -> C.CDLL:
             "psg_store_sync": ([vp, vp], i32),
             "psg_store_dump": ([vp, vp, vp], i32),
             "psg_key_list_hash": ([vp, u64, C.POINTER(u64), vp], i32),
+            "psg_store_push_frames": ([vp, C.POINTER(vp), u64, C.POINTER(vp), i32, u64, vp,
+                                       C.POINTER(i32)], i32),
+            "psg_store_push_slots_frames": ([vp, vp, u64, C.POINTER(vp), i32, u64, vp], i32),
             "psg_server_ranges": ([i32, vp, vp], i32),
             "psg_slice": ([vp, u64, vp, u64, i32, vp, vp, vp, vp, vp], i32),
             "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
@@ -368,9 +371,10 @@ class Store:
 
     def counters(self) -> dict:
         """How the store served its keyed requests (psg_store_counters)."""
-        c = (C.c_uint64 * 4)()
-        _call("psg_store_counters", self.h, c, 4)
-        return {"fused": c[0], "ident": c[1], "notident": c[2], "ordered": c[3]}
+        c = (C.c_uint64 * 6)()
+        _call("psg_store_counters", self.h, c, 6)
+        return {"fused": c[0], "ident": c[1], "notident": c[2], "ordered": c[3], "runs": c[4],
+                "run_frames": c[5]}
 
     def handle(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> None:
         _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,
@@ -386,6 +390,24 @@ class Store:
     def wait(self, ticket: int = 0) -> None:
         """Complete the requests in flight up to `ticket` (0: all); raises the first failure."""
         _call("psg_store_wait", self.h, ticket)
+
+    def push_frames(self, keys, vals, n: int, first_key: int = 0, stream=None) -> bool:
+        """A run of len(vals) Pushes on one key list (psg_store_push_frames):
+        keys is a list of device key arrays (one per request) or None for a
+        dense run; returns True when one pass served the run."""
+        k = len(vals)
+        kp = None if keys is None else (C.c_void_p * k)(*[_ptr(x) for x in keys])
+        vp_ = (C.c_void_p * k)(*[_ptr(x) for x in vals])
+        fused = C.c_int(0)
+        _call("psg_store_push_frames", self.h, kp, first_key, vp_, k, n, _s(stream), C.byref(fused))
+        return bool(fused.value)
+
+    def push_slots_frames(self, slots, vals, n: int, first: int = 0, stream=None) -> None:
+        """A run of len(vals) Pushes on a cached slot list, or (slots None) on
+        the stretch [first, first + n) (psg_store_push_slots_frames)."""
+        k = len(vals)
+        vp_ = (C.c_void_p * k)(*[_ptr(x) for x in vals])
+        _call("psg_store_push_slots_frames", self.h, _ptr(slots), first, vp_, k, n, _s(stream))
 
     def resolve(self, keys, n: int, slots, insert: bool = True, stream=None) -> None:
         _call("psg_store_resolve", self.h, _ptr(keys), n, int(insert), _ptr(slots), _s(stream))
