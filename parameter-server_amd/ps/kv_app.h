@@ -37,6 +37,7 @@
 #include "internal/PostOffice.h"
 #include "internal/customer.h"
 #include "internal/device.h"
+#include "internal/stage_time.h"
 #include "ps/base.h"
 #include "ps/range.h"
 #include "ps/simple_app.h"
@@ -198,13 +199,24 @@ class KVWorker : public SimpleApp {
            int priority = 0) {
     if (!lens.empty()) return ZPush(SVector<Key>(keys), SVector<Value>(vals), SVector<int>(lens), cmd, cb, priority);
     const bool hbm = servers_take_hbm_.load();
-    return ZPush(detail::StageFrame(keys, hbm), detail::StageFrame(vals, hbm), SVector<int>(), cmd, cb, priority);
+    SVector<Key> skeys;
+    SVector<Value> svals;
+    {
+      stage::Scope t("worker.push.copy", keys.size() * sizeof(Key) + vals.size() * sizeof(Value));
+      skeys = detail::StageFrame(keys, hbm);
+      svals = detail::StageFrame(vals, hbm);
+    }
+    return ZPush(skeys, svals, SVector<int>(), cmd, cb, priority);
   }
 
   /* KVApp.h:148-162 */
   int Pull(const std::vector<Key>& keys, std::vector<Value>* vals, std::vector<int>* lens = nullptr,
            int cmd = 0, const Callback& cb = nullptr, int priority = 0) {
-    SVector<Key> skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys, servers_take_hbm_.load());
+    SVector<Key> skeys;
+    {
+      stage::Scope t("worker.pull.copy_keys", keys.size() * sizeof(Key));
+      skeys = lens ? SVector<Key>(keys) : detail::StageFrame(keys, servers_take_hbm_.load());
+    }
     int ts = AddPullCB(skeys, vals, lens, cmd, cb);
     Data kvs;
     kvs.keys = skeys;
@@ -534,7 +546,7 @@ struct KVServerDefaultHandle {
     const size_t n = datas[0].keys.size();
     for (const auto& d : datas) {
       CHECK_EQ(d.keys.size(), n);
-      CHECK_EQ(n, d.vals.size());
+      if (!(state->key_cache && n == 1)) CHECK_EQ(n, d.vals.size());  // one value per key (KVApp.h:441)
     }
     std::vector<SVector<Value>> dvals(k);
     std::vector<const void*> vp(k);
@@ -671,6 +683,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     run = run_handle_;
   }
   CHECK(installed) << "no request handle installed 30 s after the first request";
+  stage::Scope t_recv(meta.push ? "server.request.push" : "server.request.pull");
   KVPairs<Value> data;
   const size_t n = msg.data.size();
   direct_out_ = SVector<Value>();
@@ -739,13 +752,17 @@ void KVServer<Value>::OnReceive(const Message& msg) {
   }
   detail::TraceRequest(PostOffice::Get()->my_id(), meta, data.keys.size(), 1, 0);
   // called in place: a handle keeps its state across requests (KVApp.h:457)
-  request_handle_(meta, data, this);
+  {
+    stage::Scope t("server.handle");
+    request_handle_(meta, data, this);
+  }
   direct_out_ = SVector<Value>();
   direct_taken_ = false;
 }
 
 template <typename Value>
 void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
+  stage::Scope t("server.response", res.keys.size() * sizeof(Key) + res.vals.size() * sizeof(Value));
   Message msg;
   msg.meta.app_id = customer_->app_id();
   msg.meta.customer_id = req.customer_id;
@@ -836,6 +853,7 @@ void KVWorker<Value>::DefaultSlicer(Data& send, const std::vector<Range>& ranges
 template <typename Value>
 void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const Data& kvs, bool direct,
                            const SVector<Value>* outs) {
+  stage::Scope t_send(push ? "worker.send.push" : "worker.send.pull");
   SlicedKVs sliced;
   slicer_(const_cast<Data&>(kvs), PostOffice::Get()->GetServerRanges(), &sliced);
   int skipped = 0;
@@ -960,6 +978,7 @@ int KVWorker<Value>::AddPullCB(const SVector<Key>& keys, C* vals, D* lens, int c
 template <typename Value>
 template <typename C, typename D>
 void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kvs, C* vals, D* lens) {
+  stage::Scope t_merge("worker.pull.merge", keys.size() * sizeof(Value));
   size_t total_key = 0, total_val = 0;
   int ndev = 0, ndirect = 0;
   for (const auto& r : kvs) {
@@ -995,6 +1014,7 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
   const int out_dev = detail::DeviceOf(vals);
   if (vals->empty()) {
     CHECK_LT(out_dev, 0) << "an HBM pull output must be sized by the caller";
+    stage::Scope t("worker.pull.merge.resize_output", total_val * sizeof(Value));
     vals->resize(total_val);
   } else {
     CHECK_EQ(vals->size(), total_val);
@@ -1002,6 +1022,7 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
   if (ndirect == (int)kvs.size()) {
     // every server wrote its values in place: nothing to merge
   } else if (ndev == 0 && out_dev < 0) {
+    stage::Scope t("worker.pull.merge.copy", total_val * sizeof(Value));
     Value* p = vals->data();
     for (const auto& r : kvs) {
       if (r.kv.vals.size()) HostCopy(p, r.kv.vals.data(), r.kv.vals.size() * sizeof(Value));

@@ -144,3 +144,23 @@ void ReadLocalConfigToEnv(std::string config_name) {
 }
 
 }  // namespace ps
+
+// ---- stage timing (internal/stage_time.h) -------------------------------------
+#include "internal/stage_time.h"
+#include "internal/PostOffice.h"
+
+namespace ps {
+namespace stage {
+bool On() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_STAGE_TIMES");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+void Print(const char* name, double ms, size_t bytes) {
+  PostOffice* po = PostOffice::GetIfBound();
+  std::fprintf(stderr, "[stage] node=%d %s %.3f ms %.1f MB\n", po ? po->my_id() : -1, name, ms, bytes / 1e6);
+}
+}  // namespace stage
+}  // namespace ps

@@ -57,6 +57,7 @@
 
 #include "internal/Env.h"
 #include "internal/PostOffice.h"
+#include "internal/stage_time.h"
 #include "internal/customer.h"
 #include "internal/device.h"
 #include "internal/shm_pool.h"
@@ -1091,6 +1092,7 @@ int TcpVan::Encode(const Message& msg, const Node& to, std::string* head,
 }
 
 int TcpVan::SendMsg(const Message& msg) {
+  stage::Scope t_send(msg.meta.control.cmd == Control::EMPTY ? "van.send" : "van.send.control", msg.meta.data_size);
   const int to = msg.meta.receiver;
   if (to == my_node_.id && my_node_.id != Node::kEmpty) {  // to itself: no socket
     Message m = msg;
@@ -1204,6 +1206,7 @@ void TcpVan::ReadLoop(int fd) {
     }
     std::string mb(wh.meta_bytes, '\0');
     if (!rd.read(&mb[0], mb.size())) break;
+    stage::Scope t_recv("van.recv");
     Message msg;
     try {
       Reader r{mb.data(), mb.data() + mb.size()};
