@@ -5,13 +5,14 @@
 // shared-memory blocks instead of the heap.  A frame that lies in such a block
 // is sent to a peer on the same host as (block name, offset) and the peer maps
 // the block (once, cached): the frame crosses no socket and no copy, the way
-// HBM frames travel as hipIpc mappings.  On a node with a GPU every block is
-// also registered with HIP (psg_host_register), so the server's H2D staging and
-// the D2H of a reply run at DMA rate from it.
+// HBM frames travel as hipIpc mappings.  (PS_SHM_REGISTER=1 also registers
+// every block with HIP for DMA; off by default since round 5, shm_pool.cc.)
 //
-// Names are "/psg.<pid>.<n>".  The owner unlinks its names when its Van stops
-// (and at exit); the -procs launcher removes what a crashed node left.  A block
-// that /dev/shm cannot hold is not created (posix_fallocate): the array then
+// A block is segments of at most 16 MiB ("/psg.<pid>.<n>.<k>") mapped back to
+// back; its name "/psg.<pid>.<n>:<segments>:<segment bytes>" says how to map
+// it.  The owner unlinks its names when its Van stops (and at exit); the
+// -procs launcher removes what a crashed node left.  A block that /dev/shm
+// cannot hold is not created (posix_fallocate per segment): the array then
 // comes from the heap and travels on the socket.
 #pragma once
 #include <cstddef>

@@ -105,14 +105,21 @@ SVector<T> ToDeviceAsync(const SVector<T>& v, int dev) {
 // host copy overlaps the PCIe transfer.  Otherwise — a host handle such as
 // test_kv_app_benchmark's, which would copy the frames back — or with
 // PS_STAGE_TO_HBM=0, it is the reference's host SVector copy.
+// PS_STAGE_MIN_BYTES moves the 4 MiB threshold (tests: the reference's
+// test_kv_app.cpp, 10,000 keys, then runs its CHECKs on the HBM path —
+// device slicer, HBM frames — with its own host vectors).
 template <typename T>
 SVector<T> StageFrame(const std::vector<T>& v, bool servers_take_hbm) {
   static const bool on = [] {
     const char* e = std::getenv("PS_STAGE_TO_HBM");
     return !(e && std::atoi(e) == 0);
   }();
+  static const size_t min_bytes = [] {
+    const char* e = std::getenv("PS_STAGE_MIN_BYTES");
+    return e ? (size_t)std::atoll(e) : (size_t(4) << 20);
+  }();
   const int dev = PostOffice::Get()->device();
-  if (!on || !servers_take_hbm || dev < 0 || v.size() * sizeof(T) < (size_t(4) << 20)) return SVector<T>(v);
+  if (!on || !servers_take_hbm || dev < 0 || v.empty() || v.size() * sizeof(T) < min_bytes) return SVector<T>(v);
   SVector<T> d = SVector<T>::OnDevice(v.size(), dev);
   device::StageToDevice(d.data(), v.data(), v.size() * sizeof(T));
   return d;
@@ -802,6 +809,7 @@ void KVWorker<Value>::DefaultSlicer(Data& send, const std::vector<Range>& ranges
     pos[1] = nkeys;
     vpos[1] = send.vals.size();
   } else if (send.keys.on_device()) {
+    stage::Scope t("worker.slice.device", nkeys * sizeof(Key));
     if (send.lens.size()) {
       CHECK_EQ(send.keys.size(), send.lens.size());
       CHECK(send.lens.on_device()) << "device keys need device lens";
@@ -1015,6 +1023,13 @@ void KVWorker<Value>::MergePull(const SVector<Key>& keys, std::vector<Reply>& kv
   if (vals->empty()) {
     CHECK_LT(out_dev, 0) << "an HBM pull output must be sized by the caller";
     stage::Scope t("worker.pull.merge.resize_output", total_val * sizeof(Value));
+    // the reference resizes the caller's vector (KVApp.h:703-711); its fresh
+    // pages are faulted in first, in parallel and on huge pages (PrefaultHost)
+    // — a 40 MB reply's resize took 6.4-8 ms one 4 KiB fault at a time
+    if (out_dev < 0) {
+      vals->reserve(total_val);
+      PrefaultHost(vals->data(), total_val * sizeof(Value));
+    }
     vals->resize(total_val);
   } else {
     CHECK_EQ(vals->size(), total_val);

@@ -41,6 +41,13 @@ std::shared_ptr<void> HugeAlloc(size_t bytes);
  * vector -> SVector copy of KVWorker::Push, the pull merge into the caller's
  * vector); implemented in src/device.cc. */
 void HostCopy(void* dst, const void* src, size_t bytes);
+/* memset split the same way (SVector::resize's zero fill of a large array) */
+void HostFill(void* dst, int byte, size_t bytes);
+/* first touch of a large host range the caller is about to overwrite (a
+ * std::vector the Pull merge resizes): huge pages where the range allows, then
+ * every page written in parallel, so the faults are not taken one 4 KiB page
+ * at a time by one thread; a no-op below 4 MiB */
+void PrefaultHost(void* p, size_t bytes);
 
 template <typename T>
 class SVector {
@@ -171,7 +178,15 @@ class SVector {
   void resize(size_t n, const T& val = T()) {
     size_t old = size_;
     if (n > capacity_) reserve(std::max(n, old * 2));
-    if (n > old) std::fill(data() + old, data() + n, val);
+    if (n > old) {
+      // a large zero fill (test_kv_app_benchmark's EmptyHandler answers a
+      // Pull with res.vals.resize(n)) is split over the copy threads
+      const T zero{};
+      if (!on_device() && std::memcmp(&val, &zero, sizeof(T)) == 0)
+        HostFill(data() + old, 0, (n - old) * sizeof(T));
+      else
+        std::fill(data() + old, data() + n, val);
+    }
     size_ = n;
   }
   void clear() {

@@ -122,10 +122,16 @@ std::shared_ptr<void> Alloc(size_t bytes, int dev) {
   });
 }
 
-// Pinned host blocks for large host arrays (>= 1 MiB): H2D / D2H of request
-// and reply frames then run at PCIe rate without the runtime's pageable
-// staging.  Pooled like the HBM blocks (device key -1).  Off without a GPU
-// or with PS_PINNED_HOST=0.
+// Pinned host blocks for large host arrays (>= 1 MiB): H2D / D2H of such a
+// frame then runs without the runtime's pageable staging.  Pooled like the HBM
+// blocks (device key -1).  Opt-in (PS_PINNED_HOST=1) since round 5: a size
+// class is pinned in the background the first time it is seen, and that
+// hipHostMalloc slowed the very copy it was meant to help — the cold 120 MB
+// Push of test_kv_app_benchmark took 26-35 ms with it and 2.2-2.7 ms without
+// (profiles/r5_dropin_variants.txt).  Host frames rarely reach the GPU now:
+// a worker stages its vectors into HBM itself once its servers take HBM
+// frames, and every host <-> HBM copy of the runtime goes through its own
+// pinned staging blocks (StageToDevice / StageToHost).
 std::shared_ptr<void> HostAlloc(size_t bytes) {
   // process mode: large host arrays live in shared memory, so a frame to a
   // peer process is a mapping (internal/shm_pool.h)
@@ -134,7 +140,7 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
   }
   static const bool enabled = [] {
     const char* e = std::getenv("PS_PINNED_HOST");
-    return Count() > 0 && !(e && std::atoi(e) == 0);
+    return Count() > 0 && e && std::atoi(e) != 0;
   }();
   if (!enabled || bytes < (1u << 20)) return nullptr;
   Pool& pool = GlobalPool();
@@ -172,14 +178,62 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
   });
 }
 
+// Heap blocks of >= 4 MiB on transparent huge pages, recycled: a block freed
+// by its last SVector goes back to a pool by size class (2 MiB steps) instead
+// of to the kernel, so the next frame of that size is already faulted in.  A
+// fresh block costs its first touch — 2 MiB faults, spread over the copy
+// threads of HostCopy / HostZero (120 MB: ~2 ms on the GPU host against ~10 ms
+// on 4 KiB pages, profiles/r5_probe_host_faults.txt) — and a freed one that
+// would take the pool past PS_HOST_POOL_MB (default 4096) is returned.
+namespace {
+struct HugePool {
+  std::mutex mu;
+  std::map<size_t, std::vector<void*>> free;
+  size_t held = 0;
+  size_t cap = [] {
+    const char* e = std::getenv("PS_HOST_POOL_MB");
+    const long v = e ? std::atol(e) : 4096;
+    return (size_t)(v < 0 ? 0 : v) << 20;
+  }();
+};
+HugePool& Huge() {
+  static HugePool* p = new HugePool();  // never destroyed: blocks may outlive static teardown
+  return *p;
+}
+}  // namespace
+
 std::shared_ptr<void> HugeAlloc(size_t bytes) {
   constexpr size_t kHuge = size_t(2) << 20;
   if (bytes < 2 * kHuge) return nullptr;
   const size_t rb = (bytes + kHuge - 1) & ~(kHuge - 1);
-  void* p = std::aligned_alloc(kHuge, rb);
-  if (!p) return nullptr;
-  (void)madvise(p, rb, MADV_HUGEPAGE);
-  return std::shared_ptr<void>(p, [](void* q) { std::free(q); });
+  HugePool& hp = Huge();
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(hp.mu);
+    auto it = hp.free.find(rb);
+    if (it != hp.free.end() && !it->second.empty()) {
+      p = it->second.back();
+      it->second.pop_back();
+      hp.held -= rb;
+    }
+  }
+  if (!p) {
+    p = std::aligned_alloc(kHuge, rb);
+    if (!p) return nullptr;
+    (void)madvise(p, rb, MADV_HUGEPAGE);
+  }
+  return std::shared_ptr<void>(p, [rb](void* q) {
+    HugePool& pl = Huge();
+    {
+      std::lock_guard<std::mutex> lk(pl.mu);
+      if (pl.held + rb <= pl.cap) {
+        pl.free[rb].push_back(q);
+        pl.held += rb;
+        return;
+      }
+    }
+    std::free(q);
+  });
 }
 
 void EnableAllPeerAccess() {
@@ -377,11 +431,13 @@ class CopyPool {
   explicit CopyPool(int nthreads) {
     for (int i = 0; i < nthreads; ++i) std::thread([this] { Work(); }).detach();
   }
-  void Run(char* dst, const char* src, size_t bytes, int parts, size_t chunk) {
+  /* src == nullptr: fill dst with the byte `fill` */
+  void Run(char* dst, const char* src, size_t bytes, int parts, size_t chunk, int fill = 0) {
     std::lock_guard<std::mutex> job_lk(job_mu_);
     auto job = std::make_shared<Job>();
     job->dst = dst;
     job->src = src;
+    job->fill = fill;
     job->bytes = bytes;
     job->chunk = chunk;
     job->parts = parts;
@@ -403,13 +459,17 @@ class CopyPool {
   struct Job {
     char* dst = nullptr;
     const char* src = nullptr;
+    int fill = 0;
     size_t bytes = 0, chunk = 0;
     int parts = 0;
     std::atomic<int> next{1}, left{0};
   };
   static void Part(Job& j, int i) {
     const size_t off = j.chunk * (size_t)i;
-    if (off < j.bytes) std::memcpy(j.dst + off, j.src + off, std::min(j.chunk, j.bytes - off));
+    if (off < j.bytes) {
+      if (j.src) std::memcpy(j.dst + off, j.src + off, std::min(j.chunk, j.bytes - off));
+      else std::memset(j.dst + off, j.fill, std::min(j.chunk, j.bytes - off));
+    }
     j.left.fetch_sub(1, std::memory_order_acq_rel);
   }
   static void Drain(Job& j) {
@@ -435,23 +495,55 @@ class CopyPool {
 };
 }  // namespace
 
-void HostCopy(void* dst, const void* src, size_t bytes) {
-  constexpr size_t kSplit = size_t(4) << 20;  // below this one memcpy
-  constexpr size_t kPart = size_t(1) << 20;   // smallest part handed to a worker
+namespace {
+constexpr size_t kSplit = size_t(4) << 20;  // below this one memcpy / memset
+constexpr size_t kPart = size_t(1) << 20;   // smallest part handed to a worker
+int CopyThreads() {
   static const int nthreads = [] {
     unsigned hc = std::thread::hardware_concurrency();
     const char* e = std::getenv("PS_COPY_THREADS");
     int n = e ? std::atoi(e) : (int)std::min<unsigned>(hc ? hc / 2 : 4, 8u);
     return std::max(1, n);
   }();
+  return nthreads;
+}
+CopyPool* Pool() {
+  static CopyPool* pool = new CopyPool(CopyThreads() - 1);
+  return pool;
+}
+}  // namespace
+
+void HostCopy(void* dst, const void* src, size_t bytes) {
+  const int nthreads = CopyThreads();
   if (bytes < kSplit || nthreads == 1) {
     std::memcpy(dst, src, bytes);
     return;
   }
-  static CopyPool* pool = new CopyPool(nthreads - 1);
   const int parts = (int)std::min<size_t>((size_t)nthreads, bytes / kPart);
   const size_t chunk = (bytes / parts + 4095) & ~size_t(4095);
-  pool->Run((char*)dst, (const char*)src, bytes, parts, chunk);
+  Pool()->Run((char*)dst, (const char*)src, bytes, parts, chunk);
+}
+
+void HostFill(void* dst, int byte, size_t bytes) {
+  const int nthreads = CopyThreads();
+  if (bytes < kSplit || nthreads == 1) {
+    std::memset(dst, byte, bytes);
+    return;
+  }
+  const int parts = (int)std::min<size_t>((size_t)nthreads, bytes / kPart);
+  const size_t chunk = (bytes / parts + 4095) & ~size_t(4095);
+  Pool()->Run((char*)dst, nullptr, bytes, parts, chunk, byte);
+}
+
+void PrefaultHost(void* p, size_t bytes) {
+  if (bytes < kSplit) return;
+  // the whole 2 MiB pages inside [p, p + bytes) on huge pages, then every page
+  // written once, in parallel (the caller overwrites it all anyway)
+  constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+  const uintptr_t a = ((uintptr_t)p + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t b = ((uintptr_t)p + bytes) & ~(kHuge - 1);
+  if (b > a) (void)madvise((void*)a, b - a, MADV_HUGEPAGE);
+  HostFill(p, 0, bytes);
 }
 
 }  // namespace ps

@@ -8,6 +8,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
+#include <thread>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -41,16 +44,26 @@ State& S() {
   return *s;
 }
 
+// size classes: 64 KiB steps up to 64 MiB, then 16 MiB steps (an 80 MB key
+// frame took a 128 MiB block with power-of-two classes: 60 % more to zero)
 size_t Round(size_t b) {
   if (b <= (size_t(64) << 20)) return (b + 65535) & ~size_t(65535);
-  size_t r = size_t(64) << 20;
-  while (r < b) r <<= 1;
-  return r;
+  constexpr size_t kStep = size_t(16) << 20;
+  return (b + kStep - 1) & ~(kStep - 1);
 }
 
-// pin for DMA where this process drives a GPU (best effort: unpinned still works)
+// Pin a block for DMA where this process drives a GPU — opt-in since round 5
+// (PS_SHM_REGISTER=1): hipHostRegister of a fresh 120 MB frame cost the cold
+// Push of test_kv_app_benchmark ~10-30 ms on each side (the writer's block,
+// the reader's mapping), and a host frame between processes is no longer what
+// a GPU copies from: workers stage into HBM themselves, and every host <-> HBM
+// copy of the runtime goes through its own pinned staging blocks.
 void Register(void* p, size_t n) {
-  if (device::Count() > 0) (void)psg_host_register(p, n);
+  static const bool on = [] {
+    const char* e = std::getenv("PS_SHM_REGISTER");
+    return e && std::atoi(e) != 0;
+  }();
+  if (on && device::Count() > 0) (void)psg_host_register(p, n);
 }
 }  // namespace
 
@@ -67,6 +80,83 @@ bool Enabled() {
   return S().enabled;
 }
 
+// A block is one or more POSIX shared-memory segments of at most kSeg bytes,
+// mapped back to back over one reserved address range; its name is
+// "/psg.<pid>.<n>:<segments>:<segment bytes>" and segment k is
+// "/psg.<pid>.<n>.<k>".  A fresh block's segments are reserved
+// (posix_fallocate: the pages zeroed now, so /dev/shm running out fails here,
+// not with SIGBUS at first touch) by several threads at once: tmpfs zeroes
+// one file on one thread under its inode lock, and a fresh 128 MiB block in
+// one file cost the cold Push of test_kv_app_benchmark ~15 ms in process mode
+// (profiles/r5_dropin_after2.txt).  PS_SHM_SEG_MB sets the segment size
+// (default 16).
+namespace {
+size_t SegBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("PS_SHM_SEG_MB");
+    const long mb = e ? std::atol(e) : 16;
+    return (size_t)(mb > 0 ? mb : 16) << 20;
+  }();
+  return v;
+}
+
+bool ParseName(const std::string& full, std::string* base, size_t* nseg, size_t* seg) {
+  const size_t c1 = full.find(':');
+  if (c1 == std::string::npos) return false;
+  const size_t c2 = full.find(':', c1 + 1);
+  if (c2 == std::string::npos) return false;
+  *base = full.substr(0, c1);
+  *nseg = (size_t)std::strtoull(full.c_str() + c1 + 1, nullptr, 10);
+  *seg = (size_t)std::strtoull(full.c_str() + c2 + 1, nullptr, 10);
+  return *nseg > 0 && *seg > 0;
+}
+
+// map segment k of a block at base + k * seg (creating and reserving it first
+// when `create`)
+bool MapSegment(const std::string& base_name, size_t k, size_t seg, size_t total, char* at, bool create) {
+  const std::string name = base_name + "." + std::to_string(k);
+  const size_t len = std::min(seg, total - k * seg);
+  int fd = create ? shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600) : shm_open(name.c_str(), O_RDWR, 0600);
+  if (fd < 0) return false;
+  if (create && (ftruncate(fd, (off_t)len) != 0 || posix_fallocate(fd, 0, (off_t)len) != 0)) {
+    close(fd);
+    return false;
+  }
+  void* q = mmap(at, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, 0);
+  close(fd);
+  return q == at;
+}
+
+void UnlinkBlock(const std::string& base_name, size_t nseg) {
+  for (size_t k = 0; k < nseg; ++k) shm_unlink((base_name + "." + std::to_string(k)).c_str());
+}
+
+// a block of rb bytes over nseg segments; the segments are created on up to 8
+// threads at once
+char* MapBlock(const std::string& base_name, size_t rb, size_t nseg, size_t seg, bool create) {
+  void* v = mmap(nullptr, rb, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (v == MAP_FAILED) return nullptr;
+  char* at = (char*)v;
+  std::atomic<size_t> next{0};
+  std::atomic<bool> ok{true};
+  auto work = [&] {
+    for (size_t k; (k = next.fetch_add(1)) < nseg;)
+      if (!MapSegment(base_name, k, seg, rb, at + k * seg, create)) ok = false;
+  };
+  const size_t nt = create ? std::min<size_t>(nseg, 8) : 1;
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  if (!ok) {
+    munmap(v, rb);
+    if (create) UnlinkBlock(base_name, nseg);
+    return nullptr;
+  }
+  return at;
+}
+}  // namespace
+
 std::shared_ptr<void> Alloc(size_t bytes) {
   if (bytes < kMinBytes || !Enabled()) return nullptr;
   const size_t rb = Round(bytes);
@@ -81,29 +171,18 @@ std::shared_ptr<void> Alloc(size_t bytes) {
     }
   }
   if (!p) {
-    std::string name;
+    std::string base_name;
     {
       std::lock_guard<std::mutex> lk(s.mu);
-      name = "/psg." + std::to_string(getpid()) + "." + std::to_string(s.seq++);
+      base_name = "/psg." + std::to_string(getpid()) + "." + std::to_string(s.seq++);
     }
-    int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-    if (fd < 0) return nullptr;
-    // reserve the pages now: a /dev/shm too small for the block fails here
-    // instead of with SIGBUS on first touch
-    if (ftruncate(fd, (off_t)rb) != 0 || posix_fallocate(fd, 0, (off_t)rb) != 0) {
-      close(fd);
-      shm_unlink(name.c_str());
-      return nullptr;
-    }
-    p = mmap(nullptr, rb, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (p == MAP_FAILED) {
-      shm_unlink(name.c_str());
-      return nullptr;
-    }
+    const size_t seg = SegBytes();
+    const size_t nseg = (rb + seg - 1) / seg;
+    p = MapBlock(base_name, rb, nseg, seg, true);
+    if (!p) return nullptr;
     Register(p, rb);
     std::lock_guard<std::mutex> lk(s.mu);
-    s.own[(uintptr_t)p] = Block{name, rb};
+    s.own[(uintptr_t)p] = Block{base_name + ":" + std::to_string(nseg) + ":" + std::to_string(seg), rb};
   }
   return std::shared_ptr<void>(p, [rb](void* q) {
     std::lock_guard<std::mutex> lk(S().mu);
@@ -134,20 +213,23 @@ char* Map(const std::string& name, size_t* size) {
       return it->second.first;
     }
   }
-  int fd = shm_open(name.c_str(), O_RDWR, 0600);
+  std::string base_name;
+  size_t nseg = 0, seg = 0;
+  if (!ParseName(name, &base_name, &nseg, &seg)) return nullptr;
+  // the block's size: its segments, the last one possibly shorter
+  const std::string last = base_name + "." + std::to_string(nseg - 1);
+  int fd = shm_open(last.c_str(), O_RDONLY, 0600);
   if (fd < 0) return nullptr;
   struct stat st;
-  if (fstat(fd, &st) != 0) {
-    close(fd);
-    return nullptr;
-  }
-  const size_t n = (size_t)st.st_size;
-  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  const bool got = fstat(fd, &st) == 0;
   close(fd);
-  if (p == MAP_FAILED) return nullptr;
+  if (!got) return nullptr;
+  const size_t n = (nseg - 1) * seg + (size_t)st.st_size;
+  char* p = MapBlock(base_name, n, nseg, seg, false);
+  if (!p) return nullptr;
   {
     std::lock_guard<std::mutex> lk(s.mu);
-    auto ins = s.mapped.emplace(name, std::make_pair((char*)p, n));
+    auto ins = s.mapped.emplace(name, std::make_pair(p, n));
     if (!ins.second) {  // mapped by a racing reader meanwhile: keep one
       munmap(p, n);
       *size = ins.first->second.second;
@@ -156,13 +238,17 @@ char* Map(const std::string& name, size_t* size) {
   }
   Register(p, n);
   *size = n;
-  return (char*)p;
+  return p;
 }
 
 void UnlinkAll() {
   State& s = S();
   std::lock_guard<std::mutex> lk(s.mu);
-  for (auto& kv : s.own) shm_unlink(kv.second.name.c_str());
+  for (auto& kv : s.own) {
+    std::string base_name;
+    size_t nseg = 0, seg = 0;
+    if (ParseName(kv.second.name, &base_name, &nseg, &seg)) UnlinkBlock(base_name, nseg);
+  }
 }
 
 void UnlinkOf(int pid) {

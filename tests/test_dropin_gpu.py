@@ -45,6 +45,29 @@ def test_reference_test_kv_app(ns, nw):
     assert len(errs) == nw and all(float(a) == 0 and float(b) == 0 for a, b in errs), r.stdout
 
 
+@pytest.mark.parametrize("ns,nw,procs", [(2, 1, False), (4, 2, False), (8, 1, False), (2, 2, True),
+                                         (8, 2, True)])
+def test_reference_test_kv_app_on_the_device_slicer(ns, nw, procs):
+    """The reference's test_kv_app.cpp with its own host vectors staged into
+    HBM (PS_STAGE_MIN_BYTES=1: every array once the servers said they take HBM
+    frames), so its requests are cut by the device slicer (psg_slice) into
+    HBM frames and its Pull replies are merged by psg_merge — under the
+    reference program's own CHECKs (test_kv_app.cpp:50-60).  The servers'
+    stores reject a key outside their range (PSG_ERR_RANGE), so a slice bound
+    off by one key fails the job rather than passing unnoticed."""
+    exe = os.path.join(DROPIN, "test_kv_app")
+    _need(exe)
+    args = ["-ns", ns, "-nw", nw] + (["-procs"] if procs else [])
+    r = run(exe, *args, env={"PS_STAGE_MIN_BYTES": "1", "PS_STAGE_TIMES": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    errs = re.findall(r"got error value: ([\d.eE+-]+), ([\d.eE+-]+)", r.stdout)
+    assert len(errs) == nw and all(float(a) == 0 and float(b) == 0 for a, b in errs), r.stdout
+    sliced = r.stderr.count("worker.slice.device")
+    # 50 Pushes, 1 Pull and 50 PushPulls per worker; all but the first few
+    # (before the servers' hbm_handle replies arrive) go through psg_slice
+    assert sliced >= nw * 80, (sliced, r.stderr[-2000:])
+
+
 def test_reference_multi_workers():
     exe = os.path.join(DROPIN, "test_kv_app_multi_workers")
     _need(exe)
