@@ -8,7 +8,7 @@
 // HBM frames travel as hipIpc mappings.  (PS_SHM_REGISTER=1 also registers
 // every block with HIP for DMA; off by default since round 5, shm_pool.cc.)
 //
-// A block is segments of at most 16 MiB ("/psg.<pid>.<n>.<k>") mapped back to
+// A block is segments of at most 8 MiB ("/psg.<pid>.<n>.<k>") mapped back to
 // back; its name "/psg.<pid>.<n>:<segments>:<segment bytes>" says how to map
 // it.  The owner unlinks its names when its Van stops (and at exit); the
 // -procs launcher removes what a crashed node left.  A block that /dev/shm

@@ -88,14 +88,15 @@ bool Enabled() {
 // not with SIGBUS at first touch) by several threads at once: tmpfs zeroes
 // one file on one thread under its inode lock, and a fresh 128 MiB block in
 // one file cost the cold Push of test_kv_app_benchmark ~15 ms in process mode
-// (profiles/r5_dropin_after2.txt).  PS_SHM_SEG_MB sets the segment size
-// (default 16).
+// (profiles/r5_dropin_after2.txt); in 8 MiB segments 9.8 ms, in 16 MiB ones
+// 10.3-10.9 (profiles/r5_dropin_after3.txt).  PS_SHM_SEG_MB sets the segment
+// size (default 8).
 namespace {
 size_t SegBytes() {
   static const size_t v = [] {
     const char* e = std::getenv("PS_SHM_SEG_MB");
-    const long mb = e ? std::atol(e) : 16;
-    return (size_t)(mb > 0 ? mb : 16) << 20;
+    const long mb = e ? std::atol(e) : 8;
+    return (size_t)(mb > 0 ? mb : 8) << 20;
   }();
   return v;
 }

@@ -11,9 +11,15 @@ FETCH_DIR / WRITE_DIR are the -d output directories of
   rocprofv3 --pmc FETCH_SIZE --output-format csv ...
   rocprofv3 --pmc WRITE_SIZE --output-format csv ...
 (separate passes: FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2, MI355X_MICROARCH.md
-"rocprofv3 PMC slots").  Units are KiB.  gfx950 correction (MI355X_MICROARCH.md
-"HBM"): FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming
-read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+"rocprofv3 PMC slots").  Units are KiB.  gfx950 correction, calibrated for
+every access shape the store kernels use (tools/probe_pmc_shapes.hip,
+profiles/r5_pmc_calibration.json): a read costs one TCC_EA0_RDREQ per 128-B
+line it touches and FETCH_SIZE counts 64 B of it — 16-, 8- and 4-B coalesced
+loads, every-other-word loads and 4- / 8-B gathers of one value per line alike
+— so 2 x FETCH_SIZE is the bytes of the lines read; WRITE_SIZE counts each
+write request's granule (64 B when whole 64-B halves are written, else 32 B):
+the bytes written for whole granules, the granules touched for partial ones
+(a lone 4-B store counts 32 B, a half-written 64-B half counts 64).
   hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   per launch (median).
 """
 import csv
@@ -61,7 +67,8 @@ def main():
         "fetch_size_kib_median": f,
         "write_size_kib_median": w,
         "launches": launches,
-        "correction": "gfx950: FETCH_SIZE x2 (wide streaming reads), WRITE_SIZE x1; KiB -> bytes",
+        "correction": "gfx950: FETCH_SIZE x2 = 128-B lines read, WRITE_SIZE x1 = 32/64-B write granules; "
+                      "validated per access shape (profiles/r5_pmc_calibration.json); KiB -> bytes",
         "hbm_bytes_per_launch": int(hbm),
         "alg_bytes_per_launch": alg,
         "traffic_over_alg": hbm / alg,
