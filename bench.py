@@ -64,6 +64,12 @@ WORKLOADS = {
     # one BSP round = merge the nw = 4 workers' gradient frames + the Adam update
     # (Adam.h:28-34), one kernel (psg_lr_apply_sum); a line of its own (run_lr)
     "lr": ("f32", 4, 64 << 20, 64 << 20, "LR BSP round", "LR BSP round"),
+    # the drop-in API itself (run_dropin): ZPush / ZPull through KVWorker /
+    # KVServer (KVServerDefaultHandle, HBM stores) at ns = nw = N, launched as
+    # the reference launches its harnesses (local.py: one process per node), with
+    # test_kv_app_benchmark's key layout; a line of its own
+    "dropin": ("f32", 4, 10_000_000, 10_000_000, "configs[0] layout via KVWorker/KVServer",
+               "configs[0] layout via KVWorker/KVServer"),
 }
 # algorithmic HBM bytes per key of one keyed Push on the SORTED store:
 # request key 8 + store key 8 (resolve) + value 4 + store value read/write 8
@@ -1076,6 +1082,86 @@ def run_lr(args) -> dict:
     return res
 
 
+# algorithmic HBM bytes per key of a keyed Pull on the SORTED store: request
+# key 8 + store key 8 + store value 4 + reply 4
+KEYED_PULL_BYTES = 24
+
+
+def run_dropin(args, n_gpus: int) -> dict:
+    """The drop-in API's own line: tests/harness/
+    kv_bench_dropin.cpp — HBM-resident ZPush then ZPull per step through
+    KVWorker / KVServer with KVServerDefaultHandle (src/ps/KVApp.h:234-291,
+    433-458), ns = nw = N, every node its own process as tests/local.py:87-114
+    starts them (--dropin-mode threads: every node a thread of one process, the
+    shared-GPU test mode).  Keys: test_kv_app_benchmark.cpp:47-52's
+    kMaxKey/num*i + rank (--dropin-layout 0; 1: one list shared by every worker,
+    the BSP shape whose Pushes a server serves as runs).  value = 2 * 4 B *
+    keys * N / (max over workers of the step time).  The roofline counts each
+    request's own algorithmic bytes on the general keyed path (Push 28, Pull 24
+    B per key) per GPU.  Parity: every worker checks its whole pulled vector
+    against the closed form of its integer-valued pushes, on the device."""
+    import subprocess
+    n, N = args.keys, n_gpus
+    exe = os.path.join(ROOT, "tests", "_bin", "kv_bench_dropin")
+    if not os.path.exists(exe):
+        raise SystemExit(f"{exe} not built (make -C parameter-server_amd harness)")
+    cmd = [exe, "-ns", str(N), "-nw", str(N)] + (["-procs"] if args.dropin_mode == "procs" else []) + [
+        str(n), str(args.steps), str(args.warmup), str(args.dropin_layout)]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise SystemExit(f"kv_bench_dropin failed ({r.returncode}): {r.stderr[-2000:]}")
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    workers = [l for l in lines if "rank" in l]
+    if len(workers) != N:
+        raise SystemExit(f"kv_bench_dropin: {len(workers)} worker lines for {N} workers")
+    ms = max(w["ms_per_step"] for w in workers)
+    gbs = 2 * 4 * n * N / (ms * 1e-3) / 1e9
+    try:
+        import psg as p
+        gpus = max(1, min(N, p.device_count()))
+    except Exception:
+        gpus = 1
+    # per GPU per step: its servers' N pushes and N pulls of n / N keys each
+    per_gpu = (KEYED_PUSH_BYTES + KEYED_PULL_BYTES) * n * N // gpus
+    roof = roofline(per_gpu, ms, args, "KVServerDefaultHandle requests (k_validate_windows / k_resolve_apply, "
+                    "k_ident_*, runs: k_frames_*)", 4)
+    roof["alg_bytes_note"] = (f"per GPU per step: {N} Push + {N} Pull requests of {n // N} keys per server "
+                              f"x {KEYED_PUSH_BYTES} / {KEYED_PULL_BYTES} B per key, {N // gpus if gpus else N} "
+                              "server(s) per GPU")
+    res = {
+        "metric": "device-resident KV Push+Pull GB/s (float vals) through KVWorker/KVServer",
+        "value": round(gbs, 3), "unit": "GB/s", "n_gpus": gpus, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (integer-valued U{0..99} values, generated in HBM)",
+        "config": {"workload": f"ns = nw = {N}, {n} keys per worker, "
+                               + ("test_kv_app_benchmark's keys kMaxKey/num*i + rank" if args.dropin_layout == 0
+                                  else "one key list shared by every worker (BSP: queued Pushes served as runs)"),
+                   "keys": n, "servers": N, "workers": N, "mode": args.dropin_mode,
+                   "api": "KVWorker::ZPush / ZPull (HBM SVectors), KVServerDefaultHandle",
+                   "push_ms": round(max(w["push_ms"] for w in workers), 5),
+                   "pull_ms": round(max(w["pull_ms"] for w in workers), 5)},
+        "parity_check": all(w["mismatches"] == 0 for w in workers),
+        "parity_detail": {"checked": "every worker's whole pulled vector vs the closed form of its pushes "
+                                     "(psg_verify_synth_sum)", "mismatches": [w["mismatches"] for w in workers]},
+        "roofline": roof,
+        "job_wall_s": round(wall, 2),
+    }
+    if not args.no_cpu_baseline:
+        import oracle
+        t0 = time.perf_counter()
+        f0, p0, l0 = oracle.bench(min(n, args.cpu_configs0_keys or n), 6)
+        nn = min(n, args.cpu_configs0_keys or n)
+        res["cpu_baseline"] = {"value": round(2 * 4 * nn / (p0 + l0) / 1e9, 4), "unit": "GB/s", "cores": 1,
+                               "kind": "port",
+                               "sample": (f"configs[0] layout: {nn} keys at kMaxKey/num*i through the "
+                                          f"KVServerDefaultHandle unordered_map loop, 1 inserting Push ({f0:.2f} s) "
+                                          f"then 6 Push+Pull, one thread, {time.perf_counter() - t0:.1f} s"),
+                               "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()}}
+    return res
+
+
 def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra: int = 0) -> dict:
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed PMC summaries (tools/pmc_summary.py):
@@ -1199,6 +1285,10 @@ def main(argv=None) -> None:
     ap.add_argument("--lr-frames", type=int, default=4, help="--workload lr: gradient frames per round (nw)")
     ap.add_argument("--cpu-lr-features", type=int, default=8 << 20,
                     help="--workload lr: features of the CPU baseline's sample")
+    ap.add_argument("--dropin-mode", choices=["procs", "threads"], default="procs",
+                    help="--workload dropin: one process per node (as local.py) or one thread per node")
+    ap.add_argument("--dropin-layout", type=int, choices=[0, 1], default=0,
+                    help="--workload dropin: 0 test_kv_app_benchmark's keys (+rank), 1 one shared list")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1213,6 +1303,12 @@ def main(argv=None) -> None:
         if world > 1:
             raise SystemExit("--workload lr is a one-GPU line (the N > 1 LR round is psg_comm_lr_push)")
         print(json.dumps(run_lr(args)), flush=True)
+        return
+    if args.workload == "dropin":
+        # the job launches its own nodes (one per GPU): run it from one process
+        if world > 1:
+            raise SystemExit("--workload dropin launches its own ns = nw = --gpus nodes: run it as one process")
+        print(json.dumps(run_dropin(args, args.gpus)), flush=True)
         return
     group = None
     if world > 1:

@@ -153,3 +153,20 @@ def test_configs3_keyed_cached_n4_xgmi_shared_gpu(exchange):
     assert res["config"]["keys_per_worker"] == 10_000_000 and res["n_gpus"] == 4
     assert "keyed xGMI" in res["config"]["exchange"], res["config"]
     assert ("as writes" in res["config"]["exchange"]) == exchange.endswith("-w"), res["config"]
+
+
+@pytest.mark.parametrize("n,mode,layout", [(1, "procs", 0), (2, "procs", 0), (4, "procs", 1), (8, "threads", 0),
+                                           (8, "threads", 1)])
+def test_dropin_bench_line(n, mode, layout):
+    """bench.py --workload dropin: ZPush / ZPull through KVWorker / KVServer at
+    ns = nw = n (every node on this box's one GPU), the reference's benchmark
+    key layout (0) or one shared list (1); every worker's whole pulled vector
+    is checked against the closed form of its pushes (parity_check)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "dropin", "--gpus", str(n),
+                        "--dropin-mode", mode, "--dropin-layout", str(layout), "--keys", "2000000", "--steps", "5",
+                        "--warmup", "2", "--no-cpu-baseline"], capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["parity_check"], line
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    assert line["config"]["servers"] == n and line["config"]["workers"] == n
