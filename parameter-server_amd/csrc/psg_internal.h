@@ -176,6 +176,7 @@ struct InflightReq {
   int want_land;  // a Pull answered when reaped (psg_store_handle): its reply must be in memory then
   int land;       // ... and land_ev[ring] was recorded behind its kernels to say so
   int ident;      // sent as an identity request (k_ident_check / k_ident_apply)
+  int mident;     // its validation pass marked the tiles that are stretches of the store (chunk_ok)
   int nt;         // threads per block (tile = 4 keys a lane) of its resolve-and-apply launch
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
@@ -249,6 +250,10 @@ struct psg_store {
   } wc[4];
   uint64_t wc_clock;
   uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters
+  // per request tile of the current fused Push: its request's seq when a
+  // chunk of the tile is NOT a stretch of the store (k_validate_windows); device
+  int* chunk_ok;
+  uint64_t chunk_cap;
 };
 
 struct psg_adam {

@@ -317,11 +317,25 @@ __global__ __launch_bounds__(256) void k_resolve(const uint64_t* __restrict__ q,
 // reports in the request's completion word.  Bytes: the request keys once (8 B / key, default
 // cache policy so k_resolve_apply's re-read right after can hit the Infinity
 // Cache) plus the probes.
+//
+// Tiles that are stretches of the store (round 5).  With trusted windows and
+// chunk_ok != NULL, the key-stream blocks also check, per 512-key wave chunk,
+// whether its tile's keys are exactly K[lo, lo + n_t) — the tile's window holds
+// exactly n_t store keys, its end keys are the window's, and every key equals
+// its store key — reading those store keys (8 B / key) beside the request keys
+// they already read.  A chunk that is not writes seq into its tile's word
+// chunk_ok[t]; k_resolve_apply then serves a tile whose word is not seq at
+// slots lo + i, with no key
+// re-read, no window and no search: a key list made of stretches of the store
+// (a few disjoint ranges of it) moves 8 + 8 + 4 + 8 = 28 B per key in its
+// stretch tiles, where the general path moves 36 — only the tiles that hold a
+// seam between two stretches take the general path.
 __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __restrict__ q, uint64_t n,
                                                           const uint64_t* __restrict__ K, uint64_t S,
                                                           Win* __restrict__ win, uint32_t gen, uint64_t tileN,
                                                           unsigned nsearch, uint64_t kb, uint64_t ke,
-                                                          int* __restrict__ reject, int seq, int vec) {
+                                                          int* __restrict__ reject, int seq, int vec,
+                                                          int* __restrict__ chunk_ok) {
   const uint64_t ntiles = (n + tileN - 1) / tileN;
   if (blockIdx.x < nsearch) {
     const uint64_t waves = (uint64_t)nsearch * (kBlock / 64);
@@ -397,6 +411,34 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
         if (k0[h] >= k1[h]) unsorted = 1;
       }
     }
+    if (chunk_ok && wbase < n) {
+      // is this chunk's tile a stretch of the store (see above)?  Wave-uniform
+      const uint64_t ta = wbase / tileN * tileN;
+      const uint64_t tb = ta + tileN < n ? ta + tileN : n;
+      const Win e = win[wbase / tileN];
+      bool ok = e.gen == gen && e.hi >= e.lo && (uint64_t)(e.hi - e.lo) == tb - ta && (uint64_t)e.hi <= S &&
+                e.first == q[ta] && e.last == q[tb - 1];
+      if (ok) {
+        const uint64_t kbase = (uint64_t)e.lo - ta;  // K index of request key i: kbase + i (mod 2^64)
+        bool mine = true;
+#pragma unroll
+        for (int h = 0; h < kRows; ++h) {
+          const uint64_t i = wbase + (uint64_t)h * kRowKeys + 2 * (uint64_t)lane;
+          if (i + 2 <= n && (e.lo & 1) == 0) {
+            const u64x2 c = *reinterpret_cast<const u64x2*>(K + (kbase + i));
+            mine = mine && c[0] == k0[h] && c[1] == k1[h];
+          } else {
+            if (i < n) mine = mine && K[kbase + i] == k0[h];
+            if (i + 1 < n) mine = mine && K[kbase + i + 1] == k1[h];
+          }
+        }
+        ok = __ballot(!mine) == 0;
+      }
+      // a chunk that is not marks its tile with this request's seq (every
+      // such chunk writes the same word; one that is writes nothing): a tile
+      // whose word is not this seq is a stretch of the store
+      if (lane == 0 && !ok) chunk_ok[wbase / tileN] = seq;
+    }
   }
   if (__ballot(range) && (threadIdx.x & 63) == 0) reject[kRejRange] = seq;
   if (__ballot(unsorted) && (threadIdx.x & 63) == 0) reject[kRejUnsorted] = seq;
@@ -457,7 +499,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
                                                        typename Elem<DT>::T* __restrict__ outv,
                                                        int* __restrict__ rej, int seq, int vec,
                                                        Arrival arrival, uint32_t* __restrict__ word,
-                                                       uint32_t tag_bits) {
+                                                       uint32_t tag_bits, const int* __restrict__ chunk_ok) {
   using E = Elem<DT>;
   using T = typename E::T;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
@@ -496,11 +538,21 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
   uint64_t nkey[kPerLane] = {}, nprev = 0, nqfirst = 0, nqlast = 0;
   T nv[kPerLane] = {};
   Win ne = {};
+  // a tile the validation pass found to be a stretch of the store (no chunk
+  // of it marked with this request's seq, k_validate_windows): served at
+  // slots lo + i, its keys not loaded again (block-uniform; carried in the
+  // window entry's spare word, ne.pad)
   auto load_tile = [&](uint64_t tl) {
     const uint64_t a0 = tl * tileN;
     const uint64_t a1 = (a0 + tileN < n) ? a0 + tileN : n;
     const uint64_t j0 = a0 + (uint64_t)threadIdx.x * kPerLane;
     ne = win[tl];
+    ne.pad = 0;
+    if constexpr (!CHECK) ne.pad = chunk_ok && chunk_ok[tl] != seq ? 1u : 0u;
+    if (ne.pad) {
+      nqfirst = ne.first;
+      nqlast = ne.last;
+    } else {
     nqfirst = q[a0];
     nqlast = q[a1 - 1];
     if (j0 + kPerLane <= a1 && (vec & 2)) {
@@ -515,6 +567,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
       for (int k = 0; k < kPerLane; ++k) nkey[k] = j0 + k < a1 ? q[j0 + k] : 0;
     }
     if constexpr (CHECK) nprev = ((threadIdx.x & 63) == 0 && j0 > 0 && j0 < a1) ? q[j0 - 1] : 0;
+    }
     if constexpr ((OP & PSG_PUSH) != 0) {
       bool vdone = false;
       if constexpr (sizeof(T) == 4) {
@@ -539,6 +592,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     // it was computed against this K for this tile's first and last key
     // (checked below)
     const Win e = ne;
+    const bool ident = e.pad != 0;
     const bool cur = e.gen == gen;
     uint64_t lo = cur ? e.lo : 0, hi = cur ? e.hi : 0;
     if (hi > S) hi = S;
@@ -547,7 +601,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     bool staged = W <= (uint64_t)winN;
     const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
     const bool whole = i0 + kPerLane <= t1;
-    if (cur && staged) stage_window<NT>(sK, K, lo, W);
+    if (!ident && cur && staged) stage_window<NT>(sK, K, lo, W);
     const uint64_t qfirst = nqfirst, qlast = nqlast;
     uint64_t key[kPerLane];
 #pragma unroll
@@ -582,7 +636,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     // of the window before it has landed.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!(cur && e.first == qfirst && e.last == qlast)) {
+    if (!ident && !(cur && e.first == qfirst && e.last == qlast)) {
       // stale or absent window (block-uniform): search both ends (waves 0 and
       // 1), keep the result for the next request on these keys, restage
       const int wv = threadIdx.x >> 6;
@@ -611,7 +665,14 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     uint32_t r = 0;
     uint64_t slot[kPerLane];
     bool hit[kPerLane];
-    if (staged) {
+    if (ident) {
+      // key i of the tile is K[lo + i - t0], verified by the validation pass
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        hit[k] = i0 + k < t1;
+        slot[k] = lo + (i0 + k - t0);
+      }
+    } else if (staged) {
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) {
         const uint64_t i = i0 + k;
@@ -1663,7 +1724,7 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
   arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
 #define PSG_RA_ARGS                                                                                     \
   q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end, (T*)s->vals, (const T*)vals, (T*)out, \
-      s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8
+      s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8, rec.mident ? s->chunk_ok : nullptr
   // the 256-thread tiles of a request at most 2 in 5 of whose store's keys it
   // asks for stage windows of 4 tiles (32 KiB: 4 blocks per CU instead of 8)
   // — every 3rd key of the store: Push+Pull 333 -> 361 GB/s, every 4th 266 ->
@@ -1786,10 +1847,30 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   // inside k_resolve_apply, so on trusted windows it is one launch.
   const unsigned nsearch = trusted ? 0u : (unsigned)((2 * ntiles + kBlock / 64 - 1) / (kBlock / 64));
   const unsigned nval = op == PSG_PULL || ident ? 0u : grid_n(n, (uint64_t)kBlock * 8);
+  // a validated Push on trusted windows also finds the tiles that are
+  // stretches of the store (k_validate_windows, chunk_ok); PSG_RA_MIDENT=0:
+  // never (A/B).  The flags live in one per-store array: its requests are
+  // stream-ordered, each kernel reads only the marks of its own seq.
+  static const bool mident_on = [] {
+    const char* e = getenv("PSG_RA_MIDENT");
+    return e ? atoi(e) != 0 : true;
+  }();
+  bool mident = mident_on && nval > 0 && nsearch == 0;
+  if (mident && s->chunk_cap < ntiles) {
+    if (!s->inflight.empty()) PSG_TRY(drain(s));
+    if (s->chunk_ok) PSG_HIP(hipFree(s->chunk_ok));
+    s->chunk_ok = nullptr;
+    s->chunk_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(ntiles, 4096);
+    PSG_HIP(hipMalloc(&s->chunk_ok, cap * sizeof(int)));
+    // zeroed, stream-ordered before any kernel reads it (seq is never 0)
+    PSG_HIP(hipMemsetAsync(s->chunk_ok, 0, cap * sizeof(int), st));
+    s->chunk_cap = cap;
+  }
   if (nsearch + nval > 0)
     k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
                                                          s->key_begin, s->key_end, s->reject_dev, seq,
-                                                         aligned16(q) ? 1 : 0);
+                                                         aligned16(q) ? 1 : 0, mident ? s->chunk_ok : nullptr);
   rec->ticket = ++s->next_ticket;
   if (ident && trial) wc->ident_trial = rec->ticket;
   rec->op = op;
@@ -1803,6 +1884,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   rec->wc = (int)(wc - s->wc);
   rec->stream = st;
   rec->ident = ident ? 1 : 0;
+  rec->mident = mident ? 1 : 0;
   rec->nt = nt;
   s->counters[ident ? PSG_CTR_IDENT : PSG_CTR_FUSED]++;
   if (ident) {
@@ -2347,6 +2429,7 @@ int psg_store_destroy(psg_store* s) {
   if (s->slots2) (void)hipFree(s->slots2);
   if (s->wlo) (void)hipFree(s->wlo);
   if (s->gbuf) (void)hipFree(s->gbuf);
+  if (s->chunk_ok) (void)hipFree(s->chunk_ok);
   if (s->flags_host) (void)hipHostFree(s->flags_host);
   if (s->ring_host) (void)hipHostFree(s->ring_host);
   if (s->reject_dev) (void)hipFree(s->reject_dev);

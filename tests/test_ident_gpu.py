@@ -312,3 +312,111 @@ def test_store_sync_returns_with_the_reply_in_memory():
     finally:
         psg._call("psg_host_free", host)
         s.close()
+
+
+def stretch_union(univ, m, gap, start=0):
+    """m stretches of the sorted store keys univ with `gap` store keys left out
+    between consecutive ones: a key list that is not one stretch of the store
+    (the identity request fails on it) but whose tiles mostly are."""
+    n = len(univ)
+    per = (n - start - gap * (m - 1)) // m
+    parts = [univ[start + j * (per + gap): start + j * (per + gap) + per] for j in range(m)]
+    return np.concatenate(parts)
+
+
+@pytest.mark.parametrize("dtype", [psg.F32, psg.F16])
+@pytest.mark.parametrize("m", [2, 16, 64])
+def test_stretch_union_lists_take_stretch_tiles(dtype, m):
+    """A key list made of m disjoint stretches of the store:
+    the identity attempt fails once; afterwards the general path's validation
+    pass marks every tile that is a stretch of the store (k_validate_windows,
+    chunk_ok) and k_resolve_apply serves those at slots lo + i without a key
+    re-read — seam tiles take the search.  Synchronous and in flight, every op,
+    bit-exact against the oracle."""
+    rng, univ, st, orc = populated(dtype, 400000, 91 + m)
+    k = stretch_union(univ, m, 100, start=7)
+    n = len(k)
+    dk = dev(k)
+    for r, flags in enumerate([psg.PUSH, ALL, psg.PULL, psg.PUSH, ALL, psg.PUSH]):
+        request(st, orc, dtype, flags, dk, k, 1000 * m + r)
+    c = st.counters()
+    assert c["notident"] == 1, c
+    reqs, pending = [], []
+    for j in range(12):
+        flags = [psg.PUSH, ALL, psg.PUSH, psg.PULL][j % 4]
+        v = oracle.synth(n, dtype, 2000 * m + j, 1, -1.0, 1.0)
+        dv = dev(v)
+        out = psg.DeviceBuffer(n * ES[dtype]) if flags & psg.PULL else None
+        pending.append(st.handle_async(flags, dk, dv if flags & psg.PUSH else None, out, n))
+        reqs.append((dv, out, orc.handle(flags, k, v if flags & psg.PUSH else None, n)))
+        if len(pending) > 4:
+            st.wait(pending.pop(0))
+    st.wait()
+    psg.device_sync()
+    for j, (_, out, exp) in enumerate(reqs):
+        if out is not None:
+            np.testing.assert_array_equal(out.download(NPT[dtype], n), exp, err_msg=f"request {j}")
+    same_store(st, orc, dtype)
+
+
+def test_stretch_union_list_with_a_key_out_of_range_is_rejected():
+    """A stretch-union list whose last key lies outside the shard's range: the
+    validation pass rejects the whole request (PSG_ERR_RANGE) and no tile —
+    stretch tiles included — writes anything."""
+    dtype = psg.F32
+    rng = np.random.default_rng(97)
+    ke = 1 << 62
+    univ = np.unique(rng.integers(0, ke, 200000, dtype=np.uint64))
+    st = psg.Store(psg.SORTED, dtype, 0, ke, 0)
+    orc = oracle.Store(dtype)
+    v0 = oracle.synth(len(univ), dtype, 3, 1, -1.0, 1.0)
+    st.handle(psg.PUSH, dev(univ), dev(v0), None, len(univ))
+    orc.handle(oracle.PUSH, univ, v0, len(univ))
+    k = stretch_union(univ, 8, 50)
+    dk = dev(k)
+    for r in range(3):
+        request(st, orc, dtype, psg.PUSH, dk, k, 40 + r)
+    bad = np.concatenate([k, np.array([ke + 5], np.uint64)])
+    v = oracle.synth(len(bad), dtype, 77, 1, -1.0, 1.0)
+    with pytest.raises(psg.PsgError) as ei:
+        st.handle(psg.PUSH, dev(bad), dev(v), None, len(bad))
+    assert ei.value.code == 4
+    same_store(st, orc, dtype)
+    request(st, orc, dtype, ALL, dk, k, 50)
+    same_store(st, orc, dtype)
+
+
+def test_stretch_tiles_switch_off_matches():
+    """PSG_RA_MIDENT=0 (read once per process) keeps every tile on the search
+    path: the same stretch-union sequence in fresh processes, both bit-exact."""
+    child = r"""
+import sys, numpy as np
+sys.path[:0] = {paths!r}
+import oracle, psg
+psg.set_device(0)
+rng = np.random.default_rng(63)
+univ = np.unique(rng.integers(0, (1 << 64) - 1, 300000, dtype=np.uint64))
+st, orc = psg.Store(psg.SORTED, psg.F32, 0, (1 << 64) - 1, 0), oracle.Store()
+st.handle(psg.PUSH, psg.DeviceBuffer.from_numpy(univ), psg.DeviceBuffer.from_numpy(np.ones(len(univ), np.float32)), None, len(univ))
+orc.handle(oracle.PUSH, univ, np.ones(len(univ), np.float32), len(univ))
+k = np.concatenate([univ[j * 30000 + 11: j * 30000 + 29000] for j in range(10)])
+dk = psg.DeviceBuffer.from_numpy(k)
+n = len(k)
+out = psg.DeviceBuffer(n * 4)
+for j in range(6):
+    v = oracle.synth(n, psg.F32, 70 + j, 1, -1.0, 1.0)
+    st.handle(psg.PUSH | psg.PULL, dk, psg.DeviceBuffer.from_numpy(v), out, n)
+    assert np.array_equal(out.download(np.float32, n), orc.handle(oracle.PUSH | oracle.PULL, k, v, n)), j
+gk, gv = st.dump()
+ok, ov = orc.dump()
+assert np.array_equal(gk, ok) and np.array_equal(gv, ov)
+print("ok")
+"""
+    paths = [os.path.join(os.path.dirname(HERE), "parameter-server_amd", "python"),
+             os.path.join(os.path.dirname(HERE), "oracle")]
+    for env_val in ("0", "1"):
+        env = dict(os.environ, PSG_RA_MIDENT=env_val)
+        r = subprocess.run([sys.executable, "-c", child.format(paths=paths)], env=env,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert r.stdout.strip().splitlines()[-1] == "ok"
