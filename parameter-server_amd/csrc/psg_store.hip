@@ -375,6 +375,9 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
   constexpr uint64_t kBlockKeys = (uint64_t)(kBlock / 64) * kWaveKeys;  // 2048
   for (uint64_t base = (uint64_t)(blockIdx.x - nsearch) * kBlockKeys; base < n; base += nvb * kBlockKeys) {
     const uint64_t wbase = base + (uint64_t)wv * kWaveKeys;
+    // the chunk's tile window, read first: its latency runs under the key loads
+    Win e = {};
+    if (chunk_ok && wbase < n) e = win[wbase / tileN];
     uint64_t k0[kRows], k1[kRows];
 #pragma unroll
     for (int h = 0; h < kRows; ++h) {
@@ -413,11 +416,12 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
     }
     if (chunk_ok && wbase < n) {
       // is this chunk's tile a stretch of the store (see above)?  Wave-uniform
+      // (every key of the tile equal to K[lo + i - ta] IS the tile being the
+      // stretch K[lo, lo + n_t): the window's end keys need no check; it must
+      // be of this K, and the stretch inside it)
       const uint64_t ta = wbase / tileN * tileN;
       const uint64_t tb = ta + tileN < n ? ta + tileN : n;
-      const Win e = win[wbase / tileN];
-      bool ok = e.gen == gen && e.hi >= e.lo && (uint64_t)(e.hi - e.lo) == tb - ta && (uint64_t)e.hi <= S &&
-                e.first == q[ta] && e.last == q[tb - 1];
+      bool ok = e.gen == gen && (uint64_t)e.lo + (tb - ta) <= S;
       if (ok) {
         const uint64_t kbase = (uint64_t)e.lo - ta;  // K index of request key i: kbase + i (mod 2^64)
         bool mine = true;
@@ -489,7 +493,10 @@ __device__ __forceinline__ void stage_window(uint64_t* sK, const uint64_t* __res
 // CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
 // instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
 // and the 10 M-key Pull took 56 us instead of 40.
-template <int DT, int OP, int NT, bool SP = false, int WM = 2>
+// MI: the stretch-tile form (chunk_ok, §3.1 of DESIGN.md) — a separate
+// instantiation, so the kernels that never see a stretch tile (sparse tiles,
+// Pulls) keep their registers.
+template <int DT, int OP, int NT, bool SP = false, int WM = 2, bool MI = false>
 __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const uint64_t* __restrict__ q, uint64_t n,
                                                        const uint64_t* __restrict__ K, uint64_t S,
                                                        Win* __restrict__ win, uint32_t gen, uint64_t kb,
@@ -548,7 +555,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     const uint64_t j0 = a0 + (uint64_t)threadIdx.x * kPerLane;
     ne = win[tl];
     ne.pad = 0;
-    if constexpr (!CHECK) ne.pad = chunk_ok && chunk_ok[tl] != seq ? 1u : 0u;
+    if constexpr (MI && !CHECK) ne.pad = chunk_ok[tl] != seq ? 1u : 0u;
     if (ne.pad) {
       nqfirst = ne.first;
       nqlast = ne.last;
@@ -592,7 +599,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     // it was computed against this K for this tile's first and last key
     // (checked below)
     const Win e = ne;
-    const bool ident = e.pad != 0;
+    const bool ident = MI && e.pad != 0;
     const bool cur = e.gen == gen;
     uint64_t lo = cur ? e.lo : 0, hi = cur ? e.hi : 0;
     if (hi > S) hi = S;
@@ -633,9 +640,13 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     // The window reaches LDS by DMA (global_load_lds), which only vmcnt
     // tracks; the barrier's workgroup fence does not wait on it in
     // non-tgsplit mode.  Wait explicitly so no wave reads another wave's part
-    // of the window before it has landed.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // of the window before it has landed.  (A stretch tile stages nothing: it
+    // neither waits for the loads in flight — the next tile's, prefetched —
+    // nor meets the other waves; block-uniform.)
+    if (!ident) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     if (!ident && !(cur && e.first == qfirst && e.last == qlast)) {
       // stale or absent window (block-uniform): search both ends (waves 0 and
       // 1), keep the result for the next request on these keys, restage
@@ -866,7 +877,9 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
           if (i0 + k < t1) outv[i0 + k] = o[k];
       }
     }
-    __syncthreads();
+    // the next tile may restage sK: every wave is done reading this one's
+    // (a stretch tile read none)
+    if (!ident) __syncthreads();
   }
   if (!arrived) after = block_arrive(0u, &s_cond, arrival);  // no tile (rejected, gated, or a spare block)
   request_done(after, arrival, uniform, rej + kPending, word, tag_bits);
@@ -1472,6 +1485,17 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
     if (hipMemsetAsync(e->win, 0, cap * sizeof(Win), st) != hipSuccess) return nullptr;
     e->cap_tiles = cap;
     e->trusted = 0;
+    // the stretch-tile words (k_validate_windows chunk_ok) hold one per tile of
+    // the largest entry; grown here, where the requests in flight have been
+    // drained (launch_fused), seq never 0 so zeroed words mark nothing
+    if (s->chunk_cap < cap) {
+      if (s->chunk_ok) (void)hipFree(s->chunk_ok);
+      s->chunk_ok = nullptr;
+      s->chunk_cap = 0;
+      if (hipMalloc(&s->chunk_ok, cap * sizeof(int)) != hipSuccess) return nullptr;
+      if (hipMemsetAsync(s->chunk_ok, 0, cap * sizeof(int), st) != hipSuccess) return nullptr;
+      s->chunk_cap = cap;
+    }
   }
   e->last_use = ++s->wc_clock;
   return e;
@@ -1731,7 +1755,9 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
   // 276; every 2nd keeps 2 tiles (512 against 465 with 4;
   // profiles/r4_ab_sparse_window.txt)
   const bool wide = nt == 256 && 2 * s->size >= 5 * n;
-  if (nt == 1024)
+  if (nt == 1024 && rec.mident && (OP & PSG_PUSH))
+    k_resolve_apply<DT, OP, 1024, false, 2, true><<<g, 1024, 0, st>>>(PSG_RA_ARGS);
+  else if (nt == 1024)
     k_resolve_apply<DT, OP, 1024><<<g, 1024, 0, st>>>(PSG_RA_ARGS);
   else if (nt == 256 && (vec & 4) && (OP & PSG_PUSH) && sizeof(T) == 4 && wide)
     k_resolve_apply<DT, OP, 256, true, 4><<<g, 256, 0, st>>>(PSG_RA_ARGS);
@@ -1855,18 +1881,9 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     const char* e = getenv("PSG_RA_MIDENT");
     return e ? atoi(e) != 0 : true;
   }();
-  bool mident = mident_on && nval > 0 && nsearch == 0;
-  if (mident && s->chunk_cap < ntiles) {
-    if (!s->inflight.empty()) PSG_TRY(drain(s));
-    if (s->chunk_ok) PSG_HIP(hipFree(s->chunk_ok));
-    s->chunk_ok = nullptr;
-    s->chunk_cap = 0;
-    const uint64_t cap = std::max<uint64_t>(ntiles, 4096);
-    PSG_HIP(hipMalloc(&s->chunk_ok, cap * sizeof(int)));
-    // zeroed, stream-ordered before any kernel reads it (seq is never 0)
-    PSG_HIP(hipMemsetAsync(s->chunk_ok, 0, cap * sizeof(int), st));
-    s->chunk_cap = cap;
-  }
+  // (the array grows with the window-cache entries, win_entry: never here,
+  // where a first stretch-tile request would wait for an allocation)
+  const bool mident = mident_on && nval > 0 && nsearch == 0 && nt == 1024 && s->chunk_cap >= ntiles;
   if (nsearch + nval > 0)
     k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
                                                          s->key_begin, s->key_end, s->reject_dev, seq,

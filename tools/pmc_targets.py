@@ -8,7 +8,11 @@ launch).
   adam64   k_lr_apply_sum<ADAM> on 64 M features with 4 gradient frames
            (4 x 4 B + weight 8 B + f64 moments 32 B = 56 B / feature)
 
-usage: pmc_targets.py pull256|adam64 [LAUNCHES]
+  frames8/4       a run of 8 (4) dense Pushes, 64 M floats (k_frames_apply: 8 + 4k B / element)
+  frames_keyed8/4 a run of 8 (4) Pushes of one 10 M-key list = the SORTED store (16 + 12k B / key)
+  frames_cached8/4 a run of 8 (4) Pushes on a cached stretch of slots (8 + 4k B / key)
+
+usage: pmc_targets.py TARGET [LAUNCHES]
 """
 import os
 import sys
@@ -39,6 +43,52 @@ elif what == "adam64":
     a = psg.Adam(n, 0.01)
     for it in range(reps):
         psg.lr_apply_sum(w, grads, n, 0.01, a, it, stream=s)
+elif what in ("frames8", "frames4"):
+    # a run of k dense Pushes on a 64 M-float DENSE store (k_frames_apply):
+    # store 8 + 4k B / element
+    k = int(what[-1])
+    n = 64 << 20
+    st = psg.Store(psg.DENSE, psg.F32, 0, n, n)
+    vs = [psg.DeviceBuffer(n * 4) for _ in range(k)]
+    for j, v in enumerate(vs):
+        v.fill_synth(n, psg.F32, 7 + j, 0, 0.0, 100.0, s)
+    for _ in range(reps):
+        st.push_frames(None, vs, n, stream=s)
+elif what in ("frames_keyed8", "frames_keyed4"):
+    # a run of k Pushes of one 10 M-key list (k copies of it) that is the whole
+    # SORTED store: k_frames_base + k_frames_check (store key 8 + 8 per list) +
+    # k_frames_apply (store value 8 + 4 per frame): 16 + 12k B / key
+    import numpy as np
+    k = int(what[-1])
+    n = 10_000_000
+    rng = np.random.default_rng(9)
+    keys = np.unique(rng.integers(0, (1 << 64) - 1, n + 4096, dtype=np.uint64))[:n]
+    st = psg.Store(psg.SORTED, psg.F32, 0, (1 << 64) - 1, 0)
+    dks = [psg.DeviceBuffer.from_numpy(keys, s) for _ in range(k)]
+    vs = [psg.DeviceBuffer(n * 4) for _ in range(k)]
+    for j, v in enumerate(vs):
+        v.fill_synth(n, psg.F32, 7 + j, 0, 0.0, 100.0, s)
+    st.handle(psg.PUSH, dks[0], vs[0], None, n, stream=s)
+    for _ in range(reps):
+        assert st.push_frames(dks, vs, n, stream=s)
+elif what in ("frames_cached8", "frames_cached4"):
+    # a run of k Pushes on a cached list that is a stretch of slots
+    # (psg_store_push_slots_frames, k_frames_apply): 8 + 4k B / key
+    import numpy as np
+    k = int(what[-1])
+    n = 10_000_000
+    rng = np.random.default_rng(9)
+    keys = np.unique(rng.integers(0, (1 << 64) - 1, n + 4096, dtype=np.uint64))[:n]
+    st = psg.Store(psg.SORTED, psg.F32, 0, (1 << 64) - 1, 0)
+    dk = psg.DeviceBuffer.from_numpy(keys, s)
+    slots = psg.DeviceBuffer(n * 4)
+    st.resolve(dk, n, slots, insert=True, stream=s)
+    first = st.slots_stretch(slots, n, stream=s)
+    vs = [psg.DeviceBuffer(n * 4) for _ in range(k)]
+    for j, v in enumerate(vs):
+        v.fill_synth(n, psg.F32, 7 + j, 0, 0.0, 100.0, s)
+    for _ in range(reps):
+        st.push_slots_frames(None, vs, n, first=first, stream=s)
 else:
     raise SystemExit(f"unknown target {what}")
 s.sync()
