@@ -8,6 +8,8 @@
 // HBM frames travel as hipIpc mappings.  (PS_SHM_REGISTER=1 also registers
 // every block with HIP for DMA; off by default since round 5, shm_pool.cc.)
 //
+// Frames are carved from a per-process arena built in the background at start
+// (below); a frame it cannot hold gets a block of its own.
 // A block is segments of at most 8 MiB ("/psg.<pid>.<n>.<k>") mapped back to
 // back; its name "/psg.<pid>.<n>:<segments>:<segment bytes>" says how to map
 // it.  The owner unlinks its names when its Van stops (and at exit); the
@@ -23,8 +25,10 @@
 namespace ps {
 namespace shm {
 
-/* switch the pool on for this process (process mode; PS_SHM_FRAMES=0 keeps it off) */
-void Enable();
+/* switch the pool on for this process (process mode; PS_SHM_FRAMES=0 keeps it
+   off); `arena`: build the pre-faulted frame arena in the background
+   (PS_SHM_ARENA_MB, default 256; 0 = none) — workers and servers */
+void Enable(bool arena = false);
 bool Enabled();
 /* a pooled shared-memory block of >= bytes, or nullptr (pool off / small / no room) */
 std::shared_ptr<void> Alloc(size_t bytes);

@@ -8,9 +8,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <thread>
-#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -67,12 +67,19 @@ void Register(void* p, size_t n) {
 }
 }  // namespace
 
-void Enable() {
+namespace {
+void StartArena();
+}
+
+void Enable(bool arena) {
   const char* e = std::getenv("PS_SHM_FRAMES");
-  std::lock_guard<std::mutex> lk(S().mu);
-  if (S().enabled || (e && std::atoi(e) == 0)) return;
-  S().enabled = true;
+  {
+    std::lock_guard<std::mutex> lk(S().mu);
+    if (S().enabled || (e && std::atoi(e) == 0)) return;
+    S().enabled = true;
+  }
   std::atexit([] { UnlinkAll(); });
+  if (arena) StartArena();
 }
 
 bool Enabled() {
@@ -114,7 +121,8 @@ bool ParseName(const std::string& full, std::string* base, size_t* nseg, size_t*
 
 // map segment k of a block at base + k * seg (creating and reserving it first
 // when `create`)
-bool MapSegment(const std::string& base_name, size_t k, size_t seg, size_t total, char* at, bool create) {
+bool MapSegment(const std::string& base_name, size_t k, size_t seg, size_t total, char* at, bool create,
+                bool populate) {
   const std::string name = base_name + "." + std::to_string(k);
   const size_t len = std::min(seg, total - k * seg);
   int fd = create ? shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600) : shm_open(name.c_str(), O_RDWR, 0600);
@@ -123,7 +131,7 @@ bool MapSegment(const std::string& base_name, size_t k, size_t seg, size_t total
     close(fd);
     return false;
   }
-  void* q = mmap(at, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, 0);
+  void* q = mmap(at, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED | (populate ? MAP_POPULATE : 0), fd, 0);
   close(fd);
   return q == at;
 }
@@ -133,8 +141,9 @@ void UnlinkBlock(const std::string& base_name, size_t nseg) {
 }
 
 // a block of rb bytes over nseg segments; the segments are created on up to 8
-// threads at once
-char* MapBlock(const std::string& base_name, size_t rb, size_t nseg, size_t seg, bool create) {
+// threads at once (`populate`: their page tables filled as well, for the arena)
+char* MapBlock(const std::string& base_name, size_t rb, size_t nseg, size_t seg, bool create,
+               bool populate = false) {
   void* v = mmap(nullptr, rb, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
   if (v == MAP_FAILED) return nullptr;
   char* at = (char*)v;
@@ -142,7 +151,7 @@ char* MapBlock(const std::string& base_name, size_t rb, size_t nseg, size_t seg,
   std::atomic<bool> ok{true};
   auto work = [&] {
     for (size_t k; (k = next.fetch_add(1)) < nseg;)
-      if (!MapSegment(base_name, k, seg, rb, at + k * seg, create)) ok = false;
+      if (!MapSegment(base_name, k, seg, rb, at + k * seg, create, populate)) ok = false;
   };
   const size_t nt = create ? std::min<size_t>(nseg, 8) : 1;
   std::vector<std::thread> th;
@@ -156,11 +165,112 @@ char* MapBlock(const std::string& base_name, size_t rb, size_t nseg, size_t seg,
   }
   return at;
 }
+
+// The arena: one block of PS_SHM_ARENA_MB (default 256) that a worker or
+// server builds on a background thread when its van starts — segments
+// reserved and their page tables filled (MAP_POPULATE) — and carves frames
+// from, first fit, each frame a (arena name, offset) like any other.  A fresh
+// block costs its first frame the page allocation and the write faults of
+// every page (tmpfs: the cold 120 MB Push of test_kv_app_benchmark spent
+// 9-10 ms of its 10 ms in the copy into a fresh block in process mode,
+// profiles/r5_dropin_after3.txt); the arena pays that once, off the request
+// path, while the application sets up.  A frame the arena cannot hold takes a
+// block of its own as before.
+struct Arena {
+  std::mutex mu;
+  std::thread builder;
+  bool started = false, joined = false;
+  char* base = nullptr;
+  size_t size = 0;
+  std::map<size_t, size_t> free;  // offset -> length, coalesced
+};
+Arena& A() {
+  static Arena* a = new Arena();  // never destroyed, like State
+  return *a;
+}
+
+size_t ArenaBytes() {
+  const char* e = std::getenv("PS_SHM_ARENA_MB");
+  const long mb = e ? std::atol(e) : 256;
+  return mb > 0 ? (size_t)mb << 20 : 0;
+}
+
+void BuildArena(size_t bytes) {
+  State& s = S();
+  std::string base_name;
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    base_name = "/psg." + std::to_string(getpid()) + "." + std::to_string(s.seq++);
+  }
+  const size_t seg = SegBytes();
+  const size_t nseg = (bytes + seg - 1) / seg;
+  const size_t rb = nseg * seg;
+  char* p = MapBlock(base_name, rb, nseg, seg, true, true);
+  if (!p) return;  // no room in /dev/shm: every frame takes a block of its own
+  Register(p, rb);
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    s.own[(uintptr_t)p] = Block{base_name + ":" + std::to_string(nseg) + ":" + std::to_string(seg), rb};
+  }
+  Arena& a = A();
+  a.base = p;  // published to the takers by their join of this thread
+  a.size = rb;
+  a.free[0] = rb;
+}
+
+void* ArenaTake(size_t rb) {
+  Arena& a = A();
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (!a.started) return nullptr;
+  if (!a.joined) {
+    a.builder.join();
+    a.joined = true;
+  }
+  for (auto it = a.free.begin(); it != a.free.end(); ++it) {
+    if (it->second < rb) continue;
+    const size_t off = it->first, len = it->second;
+    a.free.erase(it);
+    if (len > rb) a.free[off + rb] = len - rb;
+    return a.base + off;
+  }
+  return nullptr;
+}
+
+void ArenaGive(void* q, size_t rb) {
+  Arena& a = A();
+  std::lock_guard<std::mutex> lk(a.mu);
+  size_t off = (size_t)((char*)q - a.base), len = rb;
+  auto next = a.free.lower_bound(off);
+  if (next != a.free.end() && off + len == next->first) {
+    len += next->second;
+    next = a.free.erase(next);
+  }
+  if (next != a.free.begin()) {
+    auto prev = std::prev(next);
+    if (prev->first + prev->second == off) {
+      off = prev->first;
+      len += prev->second;
+      a.free.erase(prev);
+    }
+  }
+  a.free[off] = len;
+}
+
+void StartArena() {
+  const size_t bytes = ArenaBytes();
+  if (!bytes) return;
+  Arena& a = A();
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (a.started) return;
+  a.builder = std::thread(BuildArena, bytes);
+  a.started = true;
+}
 }  // namespace
 
 std::shared_ptr<void> Alloc(size_t bytes) {
   if (bytes < kMinBytes || !Enabled()) return nullptr;
   const size_t rb = Round(bytes);
+  if (void* q = ArenaTake(rb)) return std::shared_ptr<void>(q, [rb](void* r) { ArenaGive(r, rb); });
   State& s = S();
   void* p = nullptr;
   {
@@ -243,6 +353,14 @@ char* Map(const std::string& name, size_t* size) {
 }
 
 void UnlinkAll() {
+  {
+    Arena& a = A();  // a builder still creating segments would leave names behind
+    std::lock_guard<std::mutex> lk(a.mu);
+    if (a.started && !a.joined) {
+      a.builder.join();
+      a.joined = true;
+    }
+  }
   State& s = S();
   std::lock_guard<std::mutex> lk(s.mu);
   for (auto& kv : s.own) {

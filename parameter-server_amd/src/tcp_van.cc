@@ -1501,10 +1501,10 @@ int RunNode(const std::function<int(int, char**)>& node_main, int argc, char** a
     ::signal(SIGQUIT, DumpAllStacks);
   }
   ReadLocalConfigToEnv(argv[1]);
-  shm::Enable();
+  const Node::Role r = ParseRole(role);
+  shm::Enable(r != Node::SCHEDULER);  // the scheduler sends no large frames
   const int ns = Environment::GetIntOrDefault("PS_NUM_SERVER", 1);
   const int nw = Environment::GetIntOrDefault("PS_NUM_WORKER", 1);
-  const Node::Role r = ParseRole(role);
   g_node = new PostOffice(r, r == Node::SCHEDULER ? 0 : -1, ns, nw, -1, "tcp");
   g_node->BindThread();
   int rc = 0;
