@@ -80,6 +80,7 @@ CACHED_PUSH_BYTES = 16
 # ... and when that list's slots are a stretch of the store: value 4 + store value read/write 8
 STRETCH_PUSH_BYTES = 12
 # pushes outside warmup + steps that a run may make (calibration, verification)
+BATCHED = 20  # requests per batch of the cached-stretch line's batched timing
 EXTRA_PUSH_BOUND = 64
 
 
@@ -843,6 +844,26 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
     n_marks = max(len(sampled), 1)
     push_ms = sum(backend.elapsed(a, b) for a, b, _ in evs.values()) / n_marks
     pull_ms = sum(backend.elapsed(b, c) for _, b, c in evs.values()) / n_marks
+    batched = None
+    if world == 1 and getattr(backend, "cached", False) and getattr(backend, "stretch", None) is not None:
+        # The LR steady state's per-request cost without a marker per request
+        # (VERDICT r4 next #5): BATCHED Pushes back to back, then as many Push ->
+        # Pull steps, each batch between one pair of the same timing-only events.
+        # A marker costs ~1-2 us on ROCm, so e0 | Push | e1 charges a ~20 us
+        # Push with two of them; here they are shared by the batch.
+        a, b, c = backend.new_event(), backend.new_event(), backend.new_event()
+        backend.record(a)
+        for _ in range(BATCHED):
+            backend.push()
+        backend.record(b)
+        for _ in range(BATCHED):
+            backend.push()
+            backend.pull()
+        backend.record(c)
+        backend.sync()
+        batched = {"requests": BATCHED, "push_ms": round(backend.elapsed(a, b) / BATCHED, 5),
+                   "step_ms": round(backend.elapsed(b, c) / BATCHED, 5)}
+        extra_pushes += 2 * BATCHED
     total_pushes = args.warmup + args.steps + extra_pushes
     chk = None
     if args.check:
@@ -939,6 +960,14 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                                    "resolve found slots[i] == first + i)", vb)
         res["pull_roofline_frac"] = round(8 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         res["config"]["cached_slots"] = "stretch from slot %d" % backend.stretch
+        if batched:
+            batched["push_frac"] = round(STRETCH_PUSH_BYTES * L / (batched["push_ms"] * 1e-3) / 1e9
+                                         / HBM_PEAK_GBS, 4)
+            batched["step_gbs"] = round(2 * vb * L / (batched["step_ms"] * 1e-3) / 1e9, 1)
+            batched["what"] = (f"{BATCHED} Pushes back to back, then {BATCHED} Push -> Pull steps, each batch "
+                               "between one pair of timing-only events: the per-request cost of a steady "
+                               "request stream, dispatch included, without a marker per request")
+            res["roofline"]["batched"] = batched
     elif world == 1 and getattr(backend, "cached", False):
         res["roofline"] = roofline(CACHED_PUSH_BYTES * L, push_ms, args,
                                    "cached-slot Push: k_slots_vec (store[slot] += val, slots "
