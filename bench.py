@@ -166,6 +166,25 @@ class GpuBackend:
                 tmp.free()
                 dsk.free()
                 self.store_stretches = nstretch
+            subset = float(os.environ.get("PSG_BENCH_SUBSET", "0"))
+            if 0.0 < subset < 1.0 and self.world == 1:
+                # the request a random subset of the store at density `subset`:
+                # L (1/subset - 1) more store keys drawn uniformly (seed 10), so
+                # they fall between the request's keys at random (VERDICT r4
+                # next #4's random-subset list); no tile is a stretch
+                kk = k.astype(np.uint64)
+                m = int(round(L * (1.0 / subset - 1.0)))
+                r2 = np.random.default_rng(10)
+                more = np.setdiff1d(np.unique(r2.integers(0, (1 << 64) - 1, int(m * 1.01) + 1024, dtype=np.uint64)), kk)
+                more = r2.choice(more, m, replace=False) if len(more) > m else more
+                sk = np.unique(np.concatenate([kk, more.astype(np.uint64)]))
+                dsk = p.DeviceBuffer.from_numpy(sk)
+                tmp = p.DeviceBuffer(len(sk) * self.vb)
+                self.store.handle(p.PULL, dsk, None, tmp, len(sk), stream=self.stream)
+                self.sync()
+                tmp.free()
+                dsk.free()
+                self.store_subset = (subset, len(sk))
         else:
             self.store = p.Store(p.DENSE, self.dt, lo, lo + blk, blk)
         self.vals = p.DeviceBuffer(L * self.vb)
@@ -987,6 +1006,9 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
             # written (whole 64-B lines while 4 (e + 1) <= 64)
             e1 = backend.store_extra + 1
             res["config"]["push_min_bytes_per_key"] = 12 + 8 * e1 + 2 * min(4 * e1, 64)
+        if getattr(backend, "store_subset", None):
+            res["config"]["store_keys"] = (f"{backend.store_subset[1]} keys: the request is a random subset of the "
+                                           f"store at density {backend.store_subset[0]} (PSG_BENCH_SUBSET)")
         if getattr(backend, "store_stretches", 0):
             res["config"]["store_keys"] = (f"the request is a union of {backend.store_stretches} stretches of the "
                                            "store (4096 store keys it lacks in each seam, PSG_BENCH_STRETCHES)")

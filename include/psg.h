@@ -196,7 +196,11 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * psg_store_push_slots_frames), and the requests those runs held */
 #define PSG_CTR_RUNS 4
 #define PSG_CTR_RUN_FRAMES 5
-#define PSG_NCOUNTERS 6
+/* fused Pushes whose validation pass also resolved their tiles (coded tiles:
+ * the apply then reads no request keys and stages no window for a tile whose
+ * keys are all in the store) */
+#define PSG_CTR_CODED 6
+#define PSG_NCOUNTERS 7
 int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):

@@ -239,6 +239,7 @@ struct psg_store {
     const uint64_t* q;   // request keys (device pointer) the entry was filled for
     uint64_t n;
     void* win;           // device psg::Win[ntiles]
+    uint32_t* codes;     // device: 1024 lane codes per tile (k_validate_code), reused while they verify
     uint64_t cap_tiles;
     uint64_t last_use;
     int trusted;         // skip the search pre-pass; the kernel still verifies
@@ -250,9 +251,9 @@ struct psg_store {
   } wc[4];
   uint64_t wc_clock;
   uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters
-  // per request tile of the current fused Push: its request's seq when a
-  // chunk of the tile is NOT a stretch of the store (k_validate_windows); device
-  int* chunk_ok;
+  // per request tile of the current fused Push (device): its tile word —
+  // stretch / coded / general for the request that wrote it
+  int* chunk_ok;      // per tile: the tile word of the last request that wrote it (psg_store.hip)
   uint64_t chunk_cap;
 };
 

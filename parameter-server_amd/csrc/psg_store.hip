@@ -85,6 +85,14 @@ struct Win {
   uint32_t lo, hi, gen, pad;
 };
 
+// Tile words and lane codes (round 5, coded tiles).  tword[t] = (seq & 2^30-1)
+// << 2 | st for the request `seq`: st 2 = the tile is a stretch of the store
+// (key i at slot lo + i), 1 = a coded tile (every key found; lane l's code in
+// codes[t * 1024 + l]), 0 = the general path.  A word of another request means
+// a stretch (k_validate_windows marks only the tiles that are not).
+constexpr uint32_t kTileGeneral = 0, kTileCoded = 1, kTileStretch = 2;
+__device__ __forceinline__ uint32_t tile_tag(int seq) { return ((uint32_t)seq & 0x3fffffffu) << 2; }
+
 // Completion of a fused request and its flags, ordered by atomicity alone.
 // Every block adds ONE 64-bit value to one of 8 shard counters (blockIdx mod
 // 8, each on its own 256 B, so 2048 arrivals do not queue on one address): 1
@@ -438,10 +446,10 @@ __global__ __launch_bounds__(256) void k_validate_windows(const uint64_t* __rest
         }
         ok = __ballot(!mine) == 0;
       }
-      // a chunk that is not marks its tile with this request's seq (every
-      // such chunk writes the same word; one that is writes nothing): a tile
-      // whose word is not this seq is a stretch of the store
-      if (lane == 0 && !ok) chunk_ok[wbase / tileN] = seq;
+      // a chunk that is not marks its tile's word general for this request
+      // (every such chunk writes the same word; one that is writes nothing): a
+      // tile whose word is of another request is a stretch of the store
+      if (lane == 0 && !ok) chunk_ok[wbase / tileN] = (int)(tile_tag(seq) | kTileGeneral);
     }
   }
   if (__ballot(range) && (threadIdx.x & 63) == 0) reject[kRejRange] = seq;
@@ -489,6 +497,239 @@ __device__ __forceinline__ void stage_window(uint64_t* sK, const uint64_t* __res
   }
 }
 
+// A lane's four slots as one word: p0 = its first key's place in the tile's
+// window (13 bits: windows of at most 8192 keys), and bit d - 1 of the upper
+// 19 for each further key d places after it (its keys are ascending, so d
+// counts up; every further key within 19 places)
+constexpr uint32_t kCodeBits = 13, kCodeReach = 19;
+__device__ __forceinline__ void code_slots(uint32_t code, uint64_t lo, uint64_t* slot) {
+  slot[0] = lo + (code & ((1u << kCodeBits) - 1));
+  uint32_t m = code >> kCodeBits;
+#pragma unroll
+  for (int k = 1; k < kPerLane; ++k) {
+    slot[k] = slot[0] + 1 + (uint64_t)__builtin_ctz(m | (1u << 31));
+    m &= m - 1;
+  }
+}
+
+// A coded tile's stretch of store values V[lo, hi) (4-B values) into LDS, from
+// the 16-B aligned byte va0 <= 4 lo: whole 16-B chunks straight to LDS (as
+// stage_window), the last partial chunk's values (at most 3) through VGPRs —
+// nothing is read past 4 hi.  The caller waits (vmcnt) and meets the block.
+template <int NT>
+__device__ __forceinline__ void stage_vals(char* lds, const char* V, uint64_t va0, uint64_t vhi_b) {
+  const uint32_t nfull = (uint32_t)((vhi_b - va0) & ~15ull);
+  const char* src = V + va0;
+  for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nfull; c += (NT / 64) * 1024u) {
+    // (lanes past the whole chunks load nothing: their LDS bytes are the
+    // tail's, written below)
+    const uint32_t off = c + (threadIdx.x & 63) * 16u;
+    if (off < nfull)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + off),
+                                       (__attribute__((address_space(3))) void*)(lds + c), 16, 0, 0);
+  }
+  const uint32_t tail = (uint32_t)(vhi_b - va0) - nfull;
+  if (threadIdx.x * 4u < tail)
+    *reinterpret_cast<uint32_t*>(lds + nfull + threadIdx.x * 4u) =
+        *reinterpret_cast<const uint32_t*>(src + nfull + threadIdx.x * 4u);
+}
+
+// Pass 1 of a Push on trusted windows, coded form (PSG_RA_CODED): one 1024-thread
+// block per 4096-key tile.  The request keys are validated as in
+// k_validate_windows (strict ascent, the shard's range; reject words), and the
+// tile is RESOLVED here, where they are read anyway, instead of in the apply:
+//   - a window exactly as wide as the tile: its keys compared with K[lo + i]
+//     (8 B / key of store keys) — a stretch;
+//   - a wider one of at most 8192 keys: the lane codes cached for the tile
+//     (with the key list's windows) are verified — the store key at each coded
+//     place gathered and compared, 8 B per store key of the window — and if
+//     they no longer place every key, the window is staged into LDS, every key
+//     placed by an LDS search / gallop and, if every key is found and each
+//     lane's keys fit one code, the new lane codes (4 B per 4 keys) written.
+// k_resolve_apply<MI> then serves stretch and coded tiles from lo and the codes
+// alone — no key re-read, no window, no search: a request that is a subset of
+// its store's keys (a random 90 % of them, say) moves request key 8 + store
+// keys 8 / density + code 2 + value 4 + store values 8 / density B per key, the
+// general path 8 more (the request keys read twice).
+__global__ __launch_bounds__(1024, 8) void k_validate_code(const uint64_t* __restrict__ q, uint64_t n,
+                                                           const uint64_t* __restrict__ K, uint64_t S,
+                                                           const Win* __restrict__ win, uint32_t gen, uint64_t kb,
+                                                           uint64_t ke, int* __restrict__ reject, int seq, int vec,
+                                                           uint32_t* __restrict__ tword,
+                                                           uint32_t* __restrict__ codes) {
+  constexpr int NT = 1024;
+  constexpr uint64_t tileN = (uint64_t)NT * kPerLane;
+  constexpr uint32_t winN = 2 * NT * kPerLane;
+  __shared__ uint64_t sK[winN];
+  __shared__ uint32_t s_bad[4];  // per tile, by parity: [verify, resolve]
+  const uint64_t ntiles = (n + tileN - 1) / tileN;
+  const int lane = threadIdx.x & 63;
+  int range = 0, unsorted = 0;
+  if (threadIdx.x < 4) s_bad[threadIdx.x] = 0;
+  uint32_t it = 0;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+    const uint64_t t0 = tile * tileN;
+    const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
+    const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
+    __syncthreads();  // the previous tile's readers are done with sK and the other flags
+    if (threadIdx.x < 2) s_bad[((it + 1) & 1) * 2 + threadIdx.x] = 0;
+    uint32_t* bad = &s_bad[(it & 1) * 2];
+    // the tile's kind from its cached window alone (uniform)
+    const Win e = win[tile];
+    const bool cur = e.gen == gen && e.lo <= e.hi && (uint64_t)e.hi <= S;
+    const uint64_t lo = e.lo, W = cur ? (uint64_t)(e.hi - e.lo) : 0;
+    const uint64_t nk = t1 - t0;
+    const bool stretch = cur && W == nk, coded = cur && W > nk && W <= winN;
+    // a coded candidate's cached lane code, loaded beside the request keys
+    uint32_t cc = 0;
+    if (coded && i0 < t1) cc = codes[tile * NT + threadIdx.x];
+    uint64_t key[kPerLane];
+    if (i0 + kPerLane <= t1 && (vec & 1)) {
+      const u64x2 a = *reinterpret_cast<const u64x2*>(q + i0);
+      const u64x2 b = *reinterpret_cast<const u64x2*>(q + i0 + 2);
+      key[0] = a[0];
+      key[1] = a[1];
+      key[2] = b[0];
+      key[3] = b[1];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : 0;
+    }
+    // the store keys to compare with: a stretch tile's K[lo + i], a coded
+    // candidate's at its code's places (gathered: the same lines of K)
+    uint64_t sk[kPerLane] = {};
+    uint64_t rel[kPerLane] = {};
+    bool cok = true;
+    const uint64_t kbase = lo + (i0 - t0);
+    if (stretch) {
+      if (i0 + kPerLane <= t1 && (kbase & 1) == 0) {
+        const u64x2 a = *reinterpret_cast<const u64x2*>(K + kbase);
+        const u64x2 b = *reinterpret_cast<const u64x2*>(K + kbase + 2);
+        sk[0] = a[0];
+        sk[1] = a[1];
+        sk[2] = b[0];
+        sk[3] = b[1];
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) sk[k] = i0 + k < t1 ? K[kbase + k] : 0;
+      }
+    } else if (coded) {
+      code_slots(cc, 0, rel);
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        if (i0 + k >= t1) continue;
+        if (rel[k] < W) sk[k] = K[lo + rel[k]];
+        else cok = false;
+      }
+    }
+    {
+      // strict ascent against the key before this lane's four (the previous
+      // lane's last by a shuffle; lane 0 of a wave loads it) and the range
+      const uint64_t last = key[kPerLane - 1];
+      const uint32_t plo = __shfl_up((uint32_t)last, 1, 64), phi = __shfl_up((uint32_t)(last >> 32), 1, 64);
+      uint64_t prev = ((uint64_t)phi << 32) | plo;
+      bool have_prev = true;
+      if (lane == 0) {
+        have_prev = i0 > 0 && i0 < t1;
+        prev = have_prev ? q[i0 - 1] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        if (i0 + k < t1) {
+          if (key[k] < kb || key[k] >= ke) range = 1;
+          if (have_prev && prev >= key[k]) unsorted = 1;
+          prev = key[k];
+          have_prev = true;
+        }
+      }
+    }
+    uint32_t st = kTileGeneral;
+    if (stretch) {
+      bool mine = true;
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k)
+        if (i0 + k < t1) mine = mine && sk[k] == key[k];
+      if (__ballot(!mine) && lane == 0) bad[0] = 1;
+      __syncthreads();
+      st = bad[0] ? kTileGeneral : kTileStretch;
+    } else if (coded) {
+      // the codes cached for this tile still place every key (the steady
+      // state of a repeated key list): K at each coded place is the key, the
+      // first key at place 0 and the last at W - 1 (the window exactly the
+      // tile's: a coded tile rewrites its whole stretch of values, which must
+      // hold no other tile's keys)
+      bool ok = cok;
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        if (i0 + k >= t1) continue;
+        ok = ok && sk[k] == key[k];
+        if (i0 + k == t0) ok = ok && rel[k] == 0;
+        if (i0 + k == t1 - 1) ok = ok && rel[k] == W - 1;
+      }
+      if (__ballot(!ok) && lane == 0) bad[0] = 1;
+      __syncthreads();
+      if (!bad[0]) {
+        st = kTileCoded;
+      } else {
+        // no (valid) codes: resolve the tile in LDS and write them
+        stage_window<NT>(sK, K, lo, W);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t w = (uint32_t)W;
+        uint32_t pos[kPerLane];
+        ok = true;
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) {
+          pos[k] = 0;
+          if (i0 + k >= t1) continue;
+          const uint64_t kk = key[k];
+          if (k == 0) {
+            // with every key of the tile in its window, key i of the tile
+            // sits in [i, i + W - n_t]: a search of that bracket (its misses
+            // are tiles with absent keys, which are not coded anyway)
+            const uint32_t ri = (uint32_t)(i0 - t0), a = ri < w ? ri : w;
+            const uint32_t b = ri + (w - (uint32_t)nk) + 1 < w ? ri + (w - (uint32_t)nk) + 1 : w;
+            r = a + lower_bound_lds(sK + a, b - a, kk);
+          } else if (!(r < w && sK[r] >= kk)) {
+            // gallop forward from the previous key's place (k_resolve_apply)
+            uint32_t a = r < w ? r + 1 : w, b = a, step = 1;
+            while (b < w && sK[b] < kk) {
+              a = b + 1;
+              b = a + step;
+              step <<= 1;
+            }
+            if (b > w) b = w;
+            if (a > b) a = b;
+            r = a + lower_bound_lds(sK + a, b - a, kk);
+          }
+          ok = ok && r < w && sK[r] == kk;
+          pos[k] = r;
+        }
+        if (i0 == t0) ok = ok && pos[0] == 0;
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k)
+          if (i0 + k == t1 - 1) ok = ok && pos[k] == w - 1;
+        uint32_t code = pos[0];
+#pragma unroll
+        for (int k = 1; k < kPerLane; ++k) {
+          if (i0 + k >= t1) continue;
+          const uint32_t d = pos[k] - pos[0];
+          ok = ok && d >= 1 && d <= kCodeReach;
+          if (ok) code |= 1u << (d - 1 + kCodeBits);
+        }
+        if (i0 < t1) codes[tile * NT + threadIdx.x] = code;
+        if (__ballot(!ok) && lane == 0) bad[1] = 1;
+        __syncthreads();
+        st = bad[1] ? kTileGeneral : kTileCoded;
+      }
+    }
+    if (threadIdx.x == 0) tword[tile] = tile_tag(seq) | st;
+  }
+  if (__ballot(range) && lane == 0) reject[kRejRange] = seq;
+  if (__ballot(unsorted) && lane == 0) reject[kRejUnsorted] = seq;
+}
+
 // __launch_bounds__(NT, 8): 8 waves per SIMD, i.e. two 1024-thread blocks per
 // CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
 // instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
@@ -506,7 +747,8 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
                                                        typename Elem<DT>::T* __restrict__ outv,
                                                        int* __restrict__ rej, int seq, int vec,
                                                        Arrival arrival, uint32_t* __restrict__ word,
-                                                       uint32_t tag_bits, const int* __restrict__ chunk_ok) {
+                                                       uint32_t tag_bits, const uint32_t* __restrict__ tword,
+                                                       const uint32_t* __restrict__ codes) {
   using E = Elem<DT>;
   using T = typename E::T;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;  // request keys per block tile
@@ -544,6 +786,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
   // window, then its store values) instead of three (entry, window, values).
   uint64_t nkey[kPerLane] = {}, nprev = 0, nqfirst = 0, nqlast = 0;
   T nv[kPerLane] = {};
+  uint32_t ncode = 0;
   Win ne = {};
   // a tile the validation pass found to be a stretch of the store (no chunk
   // of it marked with this request's seq, k_validate_windows): served at
@@ -554,8 +797,12 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     const uint64_t a1 = (a0 + tileN < n) ? a0 + tileN : n;
     const uint64_t j0 = a0 + (uint64_t)threadIdx.x * kPerLane;
     ne = win[tl];
-    ne.pad = 0;
-    if constexpr (MI && !CHECK) ne.pad = chunk_ok[tl] != seq ? 1u : 0u;
+    ne.pad = kTileGeneral;
+    if constexpr (MI && !CHECK) {
+      const uint32_t tw = tword[tl];
+      ne.pad = (tw >> 2) == (tile_tag(seq) >> 2) ? (tw & 3u) : kTileStretch;
+      if (ne.pad == kTileCoded) ncode = codes[tl * NT + threadIdx.x];
+    }
     if (ne.pad) {
       nqfirst = ne.first;
       nqlast = ne.last;
@@ -609,6 +856,21 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
     const bool whole = i0 + kPerLane <= t1;
     if (!ident && cur && staged) stage_window<NT>(sK, K, lo, W);
+    // a coded tile (4-B values): its stretch of store values V[lo, hi) is
+    // staged into LDS, updated there at the coded places and written back
+    // whole — 16-B accesses to HBM where the places themselves are scattered
+    // (a random subset of the store).  The tile windows of one request are
+    // disjoint, so the slots between its keys are rewritten unchanged by the
+    // only block that touches them.
+    bool cv = false;
+    uint64_t vlo_b = 0, vhi_b = 0, va0 = 0;
+    if constexpr (MI && sizeof(T) == 4) {
+      cv = e.pad == kTileCoded;
+      vlo_b = lo * 4;
+      vhi_b = (uint64_t)e.hi * 4;
+      va0 = vlo_b & ~15ull;
+      if (cv) stage_vals<NT>(reinterpret_cast<char*>(sK), reinterpret_cast<const char*>(V), va0, vhi_b);
+    }
     const uint64_t qfirst = nqfirst, qlast = nqlast;
     uint64_t key[kPerLane];
 #pragma unroll
@@ -637,13 +899,14 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     T v[kPerLane];
 #pragma unroll
     for (int k = 0; k < kPerLane; ++k) v[k] = nv[k];
+    const uint32_t code = ncode;
     // The window reaches LDS by DMA (global_load_lds), which only vmcnt
     // tracks; the barrier's workgroup fence does not wait on it in
     // non-tgsplit mode.  Wait explicitly so no wave reads another wave's part
     // of the window before it has landed.  (A stretch tile stages nothing: it
     // neither waits for the loads in flight — the next tile's, prefetched —
     // nor meets the other waves; block-uniform.)
-    if (!ident) {
+    if (!ident || cv) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -677,12 +940,16 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     uint64_t slot[kPerLane];
     bool hit[kPerLane];
     if (ident) {
-      // key i of the tile is K[lo + i - t0], verified by the validation pass
+      // key i of the tile is K[lo + i - t0] (a stretch), or at the places its
+      // lane's code gives (a coded tile), as the validation pass found
+      if (e.pad == kTileCoded) {
+        code_slots(code, lo, slot);
+      } else {
 #pragma unroll
-      for (int k = 0; k < kPerLane; ++k) {
-        hit[k] = i0 + k < t1;
-        slot[k] = lo + (i0 + k - t0);
+        for (int k = 0; k < kPerLane; ++k) slot[k] = lo + (i0 + k - t0);
       }
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) hit[k] = i0 + k < t1;
     } else if (staged) {
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) {
@@ -806,7 +1073,13 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
                 sbase + 8 <= S && prev_hi < sbase && next_lo >= sbase + 8;
       }
     }
-    if (span8) {
+    if (cv) {
+      if constexpr (MI && sizeof(T) == 4) {
+        const T* sV = reinterpret_cast<const T*>(reinterpret_cast<const char*>(sK) + (vlo_b - va0));
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) x[k] = hit[k] ? sV[slot[k] - lo] : (T)0.0f;
+      }
+    } else if (span8) {
       if constexpr (sizeof(T) == 4 && (OP & PSG_PUSH) != 0) {
         sa = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + sbase));
         sb = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + sbase + 4));
@@ -839,7 +1112,33 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
       if constexpr ((OP & PSG_PUSH) != 0) o[k] = E::add1(x[k], v[k]);
     }
     if constexpr ((OP & PSG_PUSH) != 0) {
-      if (span8) {
+      if (cv) {
+        if constexpr (MI && sizeof(T) == 4) {
+          T* sV = reinterpret_cast<T*>(reinterpret_cast<char*>(sK) + (vlo_b - va0));
+#pragma unroll
+          for (int k = 0; k < kPerLane; ++k)
+            if (hit[k]) sV[slot[k] - lo] = o[k];
+          __syncthreads();
+          // write the stretch back: whole 16-B chunks inside [lo, hi) as
+          // vectors, the partial first and last chunks value by value
+          const uint32_t nbytes = (uint32_t)(vhi_b - va0);
+          char* Vb = reinterpret_cast<char*>(V);
+          const char* sb = reinterpret_cast<const char*>(sK);
+          for (uint32_t c = threadIdx.x * 16u; c < nbytes; c += NT * 16u) {
+            const uint64_t gb = va0 + c;
+            if (gb >= vlo_b && c + 16u <= nbytes) {
+              *reinterpret_cast<u32x4*>(Vb + gb) = *reinterpret_cast<const u32x4*>(sb + c);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const uint64_t b = gb + 4u * j;
+                if (b >= vlo_b && b < vhi_b)
+                  *reinterpret_cast<uint32_t*>(Vb + b) = *reinterpret_cast<const uint32_t*>(sb + c + 4u * j);
+              }
+            }
+          }
+        }
+      } else if (span8) {
         if constexpr (sizeof(T) == 4) {
 #pragma unroll
           for (int k = 0; k < kPerLane; ++k) {
@@ -879,7 +1178,7 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     }
     // the next tile may restage sK: every wave is done reading this one's
     // (a stretch tile read none)
-    if (!ident) __syncthreads();
+    if (!ident || cv) __syncthreads();
   }
   if (!arrived) after = block_arrive(0u, &s_cond, arrival);  // no tile (rejected, gated, or a spare block)
   request_done(after, arrival, uniform, rej + kPending, word, tag_bits);
@@ -1476,10 +1775,16 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
   }
   if (e->cap_tiles < ntiles) {
     if (e->win) (void)hipFree(e->win);
+    if (e->codes) (void)hipFree(e->codes);
     e->win = nullptr;
+    e->codes = nullptr;
     e->cap_tiles = 0;
     const uint64_t cap = std::max<uint64_t>(ntiles, 64);
     if (hipMalloc(&e->win, cap * sizeof(Win)) != hipSuccess) return nullptr;
+    // the lane codes of its coded tiles (k_validate_code), kept with the
+    // windows and verified by every request that uses them; without them the
+    // stretch check alone runs
+    if (hipMalloc(&e->codes, cap * 1024 * sizeof(uint32_t)) != hipSuccess) e->codes = nullptr;
     // gen 0 never matches a store generation: a fresh entry is all misses
     // (stream-ordered before the request's kernels, which fill it)
     if (hipMemsetAsync(e->win, 0, cap * sizeof(Win), st) != hipSuccess) return nullptr;
@@ -1748,7 +2053,8 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
   arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
 #define PSG_RA_ARGS                                                                                     \
   q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end, (T*)s->vals, (const T*)vals, (T*)out, \
-      s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8, rec.mident ? s->chunk_ok : nullptr
+      s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8,                           \
+      rec.mident ? (const uint32_t*)s->chunk_ok : nullptr, s->wc[rec.wc].codes
   // the 256-thread tiles of a request at most 2 in 5 of whose store's keys it
   // asks for stage windows of 4 tiles (32 KiB: 4 blocks per CU instead of 8)
   // — every 3rd key of the store: Push+Pull 333 -> 361 GB/s, every 4th 266 ->
@@ -1884,7 +2190,20 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   // (the array grows with the window-cache entries, win_entry: never here,
   // where a first stretch-tile request would wait for an allocation)
   const bool mident = mident_on && nval > 0 && nsearch == 0 && nt == 1024 && s->chunk_cap >= ntiles;
-  if (nsearch + nval > 0)
+  // ... and resolves the tiles that are subsets of their windows there too
+  // (k_validate_code; PSG_RA_CODED=0: the stretch check alone, A/B)
+  static const bool coded_on = [] {
+    const char* e = getenv("PSG_RA_CODED");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (mident && coded_on && wc->codes) {
+    const unsigned cus = (unsigned)(max_stream_blocks() / 8);
+    const unsigned gcode = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
+    k_validate_code<<<gcode, 1024, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end,
+                                            s->reject_dev, seq, aligned16(q) ? 1 : 0, (uint32_t*)s->chunk_ok,
+                                            wc->codes);
+    s->counters[PSG_CTR_CODED]++;
+  } else if (nsearch + nval > 0)
     k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
                                                          s->key_begin, s->key_end, s->reject_dev, seq,
                                                          aligned16(q) ? 1 : 0, mident ? s->chunk_ok : nullptr);
@@ -2454,8 +2773,10 @@ int psg_store_destroy(psg_store* s) {
   if (s->done_ev) (void)hipEventDestroy(s->done_ev);
   for (hipEvent_t ev : s->land_ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (auto& c : s->wc)
+  for (auto& c : s->wc) {
     if (c.win) (void)hipFree(c.win);
+    if (c.codes) (void)hipFree(c.codes);
+  }
   delete s;
   return PSG_OK;
 }
