@@ -516,8 +516,11 @@ struct KVServerDefaultHandle {
       SVector<Value> dvals;
       if (req_meta.push) dvals = detail::ToDeviceAsync(req_data.vals, dev);
       if (req_meta.pull) dout = PullOutput(server, n, dev, &direct);
-      device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
-                    "psg_store_handle");
+      {
+        stage::Scope t(req_meta.push ? "server.handle.store.push" : "server.handle.store.pull");
+        device::Check(psg_store_handle(state->store, flags, dkeys.data(), 0, dvals.data(), dout.data(), n, s),
+                      "psg_store_handle");
+      }
       // psg_store_handle returns once the request's keys and vals are no longer
       // read and a Pull's reply is in memory (psg.h), so it can be answered
       // now.  Later requests on this thread's stream are ordered behind it.
