@@ -45,6 +45,21 @@ def test_svector_semantics():
     assert "svector ok" in r.stdout
 
 
+def test_shm_frame_arena():
+    """The process-mode frame arena (src/shm_pool.cc): live frames never
+    overlap under random churn, freed ranges coalesce, a full arena and an
+    oversized frame fall back to blocks of their own, a peer's mapping by name
+    shows a frame's bytes, and nothing is left in /dev/shm."""
+    exe = os.path.join(BIN, "shm_arena_unit")
+    _need(exe)
+    before = {f for f in os.listdir("/dev/shm") if f.startswith("psg.")}
+    r = run(exe, env={"PS_SHM_ARENA_MB": "16"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "shm arena ok" in r.stdout
+    after = {f for f in os.listdir("/dev/shm") if f.startswith("psg.")}
+    assert after <= before, sorted(after - before)
+
+
 @pytest.mark.parametrize("ns,nw", [(1, 1), (2, 1), (3, 2), (8, 4)])
 def test_host_cluster(ns, nw):
     exe = os.path.join(BIN, "kv_cluster_host")
