@@ -243,14 +243,18 @@ bool all_aligned(const void* const* p, int k) {
   return true;
 }
 
-// PSG_FRAMES_BPC (A/B): blocks of 256 per CU of the frame kernels (default 8)
-int frames_bpc() {
+// Blocks of 256 per CU of the frame kernels: 8 for a run over at most 64 MiB
+// of store values, 2 past it — k = 8 frames on 64 M floats took 437 us at 2
+// against 452-474 at 4-16, on 10 M 67-69 us at any (profiles/r5_frames_bpc_sweep.txt).
+// PSG_FRAMES_BPC (A/B) sets it for every size.
+int frames_bpc(uint64_t store_bytes) {
   static const int v = [] {
     const char* e = getenv("PSG_FRAMES_BPC");
     const int b = e ? atoi(e) : 0;
-    return b >= 1 && b <= 16 ? b : 8;
+    return b >= 1 && b <= 16 ? b : 0;
   }();
-  return v;
+  if (v) return v;
+  return store_bytes > (64ull << 20) ? 2 : 8;
 }
 
 template <int DT>
@@ -262,7 +266,7 @@ int apply_t(void* store_vals, uint64_t store_elems, const void* const* vals, int
   const int vec = aligned16(store_vals) && all_aligned(vals, k) ? 1 : 0;
   // past the Infinity Cache the store is read and written once: non-temporal
   const int nt = (uint64_t)sizeof(T) * store_elems > (512ull << 20) ? 2 : 0;
-  const unsigned g = frames_grid(vec ? n / Elem<DT>::kVec : n, frames_bpc());
+  const unsigned g = frames_grid(vec ? n / Elem<DT>::kVec : n, frames_bpc(n * sizeof(T)));
   return by_maxf(k, [&](auto mc) -> int {
     constexpr int M = decltype(mc)::value;
     if (nt)
@@ -281,7 +285,7 @@ int slots_t(void* store_vals, const uint32_t* slots, const void* const* vals, in
   FramePtrs f = {};
   for (int j = 0; j < k; ++j) f.p[j] = vals[j];
   const int vec = sizeof(T) == 4 && aligned16(slots) && all_aligned(vals, k) ? 1 : 0;
-  const unsigned g = frames_grid(vec ? n / 4 : n, frames_bpc());
+  const unsigned g = frames_grid(vec ? n / 4 : n, frames_bpc(0));
   return by_maxf(k, [&](auto mc) -> int {
     constexpr int M = decltype(mc)::value;
     k_frames_slots<DT, M><<<g, kBlock, 0, st>>>((T*)store_vals, slots, f, k, n, vec, rej, seq, flag);
@@ -307,7 +311,7 @@ int frames_check(const uint64_t* ref, const uint64_t* base, const uint64_t* cons
     f.p[j] = keys[j];
     if (j >= j0) vec = vec && aligned16(keys[j]);
   }
-  const unsigned g = frames_grid(vec ? n / 2 : n, frames_bpc());
+  const unsigned g = frames_grid(vec ? n / 2 : n, frames_bpc(0));
   return by_maxf(k, [&](auto mc) -> int {
     constexpr int M = decltype(mc)::value;
     k_frames_check<M><<<g, kBlock, 0, st>>>(ref, base, f, j0, k, n, vec ? 1 : 0, rej, seq);
