@@ -1020,13 +1020,14 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "requests in flight, each reporting completion and flags in one "
                      "kernel-written word; one server, so no slicer pass)")
         else:
-            kname = ("SORTED-store Push: k_validate_windows + k_resolve_apply "
-                     "(whole-request validation before any write, which also marks the "
-                     "tiles that are stretches of the store: those are applied at slots "
-                     "lo + i without a key re-read or a window; tile windows "
-                     "cached per key array; requests in flight, each reporting "
-                     "completion and flags in one kernel-written word; one "
-                     "server, so no slicer pass)")
+            kname = ("SORTED-store Push: k_validate_code + k_resolve_apply "
+                     "(whole-request validation before any write, which also sorts the "
+                     "tiles on trusted windows: stretches of the store are applied at "
+                     "slots lo + i, subsets of their window at places from lane codes "
+                     "cached with the windows and verified each request — neither "
+                     "re-reads its keys or searches; other tiles search their window "
+                     "in LDS; requests in flight, each reporting completion and flags "
+                     "in one kernel-written word; one server, so no slicer pass)")
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args, kname, vb,
                                    store_extra=getattr(backend, "store_extra", 0))
         res["pull_roofline_frac"] = round(24 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
