@@ -1019,6 +1019,12 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "key, 16 B/key — is the whole validation, then values only, 12 B/key; "
                      "requests in flight, each reporting completion and flags in one "
                      "kernel-written word; one server, so no slicer pass)")
+        elif paths.get("coded", 0) == 0:
+            kname = ("SORTED-store Push: k_validate_windows + k_resolve_apply "
+                     "(whole-request validation before any write; each tile searches "
+                     "its window in LDS; tile windows cached per key array; requests "
+                     "in flight, each reporting completion and flags in one "
+                     "kernel-written word; one server, so no slicer pass)")
         else:
             kname = ("SORTED-store Push: k_validate_code + k_resolve_apply "
                      "(whole-request validation before any write, which also sorts the "
@@ -1028,8 +1034,17 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "re-reads its keys or searches; other tiles search their window "
                      "in LDS; requests in flight, each reporting completion and flags "
                      "in one kernel-written word; one server, so no slicer pass)")
+        # the store layout the PMC summary must have been taken on (a random
+        # subset moves more lines than a union of stretches)
+        layout = ""
+        if getattr(backend, "store_subset", None):
+            layout = f"subset{backend.store_subset[0]}"
+        elif getattr(backend, "store_stretches", 0):
+            layout = f"stretch{backend.store_stretches}"
+        elif not getattr(backend, "store_extra", 0) and not (paths["ident"] > 0 and paths["notident"] == 0):
+            layout = "general"
         res["roofline"] = roofline(KEYED_PUSH_BYTES * L, push_ms, args, kname, vb,
-                                   store_extra=getattr(backend, "store_extra", 0))
+                                   store_extra=getattr(backend, "store_extra", 0), layout=layout)
         res["pull_roofline_frac"] = round(24 * L / (pull_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     elif world == 1:
         res["roofline"] = roofline(PUSH_ACCESSES * vb * blk, push_ms, args,
@@ -1247,7 +1262,8 @@ def run_dropin(args, n_gpus: int) -> dict:
     return res
 
 
-def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra: int = 0) -> dict:
+def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra: int = 0,
+             layout: str = "") -> dict:
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     # HBM bytes per launch from the committed PMC summaries (tools/pmc_summary.py):
     # the one measured on this kernel at these algorithmic bytes and on this
@@ -1263,7 +1279,7 @@ def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra:
             continue
         names = [k.split("<")[0].strip() for k in str(d.get("kernel", "")).split("|")]
         if (d.get("alg_bytes_per_launch") == alg_bytes and d.get("store_extra", 0) == store_extra and names
-                and all(n in kernel for n in names)):
+                and d.get("store_layout", "") == layout and all(n in kernel for n in names)):
             traffic = d.get("hbm_bytes_per_launch")
             source = os.path.relpath(pmc, ROOT)
             break
