@@ -1781,10 +1781,8 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
     e->cap_tiles = 0;
     const uint64_t cap = std::max<uint64_t>(ntiles, 64);
     if (hipMalloc(&e->win, cap * sizeof(Win)) != hipSuccess) return nullptr;
-    // the lane codes of its coded tiles (k_validate_code), kept with the
-    // windows and verified by every request that uses them; without them the
-    // stretch check alone runs
-    if (hipMalloc(&e->codes, cap * 1024 * sizeof(uint32_t)) != hipSuccess) e->codes = nullptr;
+    // (the lane codes of its coded tiles, 1 B per key, are allocated with
+    // the first Push that validates them: launch_fused)
     // gen 0 never matches a store generation: a fresh entry is all misses
     // (stream-ordered before the request's kernels, which fill it)
     if (hipMemsetAsync(e->win, 0, cap * sizeof(Win), st) != hipSuccess) return nullptr;
@@ -2196,6 +2194,14 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     const char* e = getenv("PSG_RA_CODED");
     return e ? atoi(e) != 0 : true;
   }();
+  // the entry's lane codes (k_validate_code), kept with its windows and
+  // verified by every request that uses them: allocated for the first Push
+  // that validates coded tiles on it (without them, the stretch check alone)
+  if (mident && coded_on && !wc->codes &&
+      hipMalloc(&wc->codes, wc->cap_tiles * 1024 * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    wc->codes = nullptr;
+  }
   if (mident && coded_on && wc->codes) {
     const unsigned cus = (unsigned)(max_stream_blocks() / 8);
     const unsigned gcode = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
