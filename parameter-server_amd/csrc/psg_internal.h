@@ -178,6 +178,9 @@ struct InflightReq {
   int ident;      // sent as an identity request (k_ident_check / k_ident_apply)
   int mident;     // its validation pass marked the tiles that are stretches of the store (chunk_ok)
   int nt;         // threads per block (tile = 4 keys a lane) of its resolve-and-apply launch
+  int seq;        // its sequence number (reject words, tile words)
+  uint32_t tw_ring;  // the ring slot whose tile words its validation wrote (a follow-up keeps it)
+  int lean;       // applied by k_tile_apply (its stretch and coded tiles; general ones follow up)
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
 }  // namespace psg
@@ -248,13 +251,14 @@ struct psg_store {
     uint32_t ident_ok;   // K's generation at which an identity request on this list completed as one
     uint64_t ident_trial;  // ticket of the identity attempt in flight before either is known (0: none)
     int nt;              // the block size (tile size / 4) its windows were filled for
+    uint32_t lean_fail;  // K's generation at which a k_tile_apply on this list left general tiles
   } wc[4];
   uint64_t wc_clock;
   uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters
   // per request tile of the current fused Push (device): its tile word —
   // stretch / coded / general for the request that wrote it
-  int* chunk_ok;      // per tile: the tile word of the last request that wrote it (psg_store.hip)
-  uint64_t chunk_cap;
+  int* chunk_ok;      // per ring slot, per tile: the tile words of the request in that slot (psg_store.hip)
+  uint64_t chunk_cap;  // tiles per ring slot
 };
 
 struct psg_adam {

@@ -64,7 +64,7 @@ __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
 // The fused keyed request (k_resolve_apply) reports through ONE word of the
 // store's ring in pinned host memory: bits [8, 32) the request's 24-bit tag,
 // bits [0, 8) its flags:
-enum { W_MISSING = 1, W_WINMISS = 2, W_RANGE = 4, W_UNSORTED = 8, W_GATED = 16, W_NOTIDENT = 32 };
+enum { W_MISSING = 1, W_WINMISS = 2, W_RANGE = 4, W_UNSORTED = 8, W_GATED = 16, W_NOTIDENT = 32, W_PARTIAL = 64 };
 // Device words (reject_dev): the validation pass writes a request's sequence
 // number into [kRejRange] / [kRejUnsorted] when a key is out of the shard's
 // range / out of order.  [kPending] != 0: an earlier request needs the host
@@ -90,7 +90,7 @@ struct Win {
 // (key i at slot lo + i), 1 = a coded tile (every key found; lane l's code in
 // codes[t * 1024 + l]), 0 = the general path.  A word of another request means
 // a stretch (k_validate_windows marks only the tiles that are not).
-constexpr uint32_t kTileGeneral = 0, kTileCoded = 1, kTileStretch = 2;
+constexpr uint32_t kTileGeneral = 0, kTileCoded = 1, kTileStretch = 2, kTileDone = 3;
 __device__ __forceinline__ uint32_t tile_tag(int seq) { return ((uint32_t)seq & 0x3fffffffu) << 2; }
 
 // Completion of a fused request and its flags, ordered by atomicity alone.
@@ -177,7 +177,7 @@ __device__ __forceinline__ void request_done(uint64_t after, const Arrival& a, u
   // all of a counter's accesses); the set is next used kRing requests later
   for (int k = 0; k <= kArriveShards; ++k)
     (void)__hip_atomic_exchange(a.ctr + k * kArriveStride, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!(f & (W_GATED | W_RANGE)) && (f & (W_MISSING | W_UNSORTED | W_NOTIDENT)))
+  if (!(f & (W_GATED | W_RANGE)) && (f & (W_MISSING | W_UNSORTED | W_NOTIDENT | W_PARTIAL)))
     __hip_atomic_store(pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(word, tag_bits | f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -730,6 +730,136 @@ __global__ __launch_bounds__(1024, 8) void k_validate_code(const uint64_t* __res
   if (__ballot(unsorted) && lane == 0) reject[kRejUnsorted] = seq;
 }
 
+// The apply of a Push whose validation pass (k_validate_code) sorted its tiles,
+// for the tiles that need no search: a stretch at slots lo + i, a coded tile at
+// the places of its lane codes, its stretch of values staged into LDS, updated
+// and written back whole (as k_resolve_apply<MI> does) — a kernel of its own,
+// without the general path's window staging and search, so it keeps more in
+// flight than the one instantiation that serves every kind.  Speculative, like
+// the identity requests: the host sends a list here while its last attempt
+// left no general tile; a general tile is left to k_resolve_apply<MI>, which
+// the host launches as the follow-up (the word reports W_PARTIAL and raises
+// kPending) and which then serves only the general tiles (vec bit 8).  (The
+// tile words are only read here: each wave reads its tile's word itself.)
+// 4-byte values.
+template <int DT, int OP>
+__global__ __launch_bounds__(1024, 8) void k_tile_apply(uint64_t n, const Win* __restrict__ win,
+                                                        typename Elem<DT>::T* __restrict__ V,
+                                                        const typename Elem<DT>::T* __restrict__ vals,
+                                                        typename Elem<DT>::T* __restrict__ outv, int* __restrict__ rej,
+                                                        int seq, int vec, Arrival arrival, uint32_t* __restrict__ word,
+                                                        uint32_t tag_bits, const uint32_t* __restrict__ tword,
+                                                        const uint32_t* __restrict__ codes) {
+  using E = Elem<DT>;
+  using T = typename E::T;
+  static_assert(sizeof(T) == 4, "4-byte values");
+  constexpr int NT = 1024;
+  constexpr uint64_t tileN = (uint64_t)NT * kPerLane;
+  __shared__ uint32_t sV[2 * NT * kPerLane + 8];  // a coded tile's values (windows of at most 8192 keys)
+  __shared__ uint32_t s_cond;
+  if (threadIdx.x == 0) s_cond = 0;
+  __syncthreads();
+  uint32_t uniform = rej[kPending] != 0 ? (uint32_t)W_GATED : 0u;
+  if (rej[kRejRange] == seq) uniform |= W_RANGE;
+  if (rej[kRejUnsorted] == seq) uniform |= W_UNSORTED;
+  const uint64_t ntiles = uniform ? 0 : (n + tileN - 1) / tileN;
+  const uint32_t tag = tile_tag(seq);
+  int partial = 0;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * tileN;
+    const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
+    const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
+    const uint32_t tw = tword[tile];
+    const uint32_t st = (tw >> 2) == (tag >> 2) ? (tw & 3u) : kTileGeneral;
+    if (st != kTileStretch && st != kTileCoded) {  // (uniform) the follow-up's
+      partial = 1;
+      continue;
+    }
+    const Win e = win[tile];
+    const uint64_t lo = e.lo;
+    const bool whole = i0 + kPerLane <= t1;
+    T v[kPerLane];
+    if (whole && (vec & 1)) {
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + i0)));
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) v[k] = i0 + k < t1 ? vals[i0 + k] : (T)0.0f;
+    }
+    T o[kPerLane];
+    if (st == kTileStretch) {
+      const uint64_t s0 = lo + (i0 - t0);
+      if (whole && (s0 & 3) == 0) {
+        f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + s0));
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) {
+          o[k] = E::add1(x[k], v[k]);
+          x[k] = o[k];
+        }
+        *reinterpret_cast<u32x4*>(V + s0) = __builtin_bit_cast(u32x4, x);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) {
+          o[k] = (T)0.0f;
+          if (i0 + k < t1) {
+            o[k] = E::add1(V[s0 + k], v[k]);
+            V[s0 + k] = o[k];
+          }
+        }
+      }
+    } else {
+      // the tile's stretch of values V[lo, hi) in LDS from the 16-B aligned
+      // byte va0, updated at the coded places, written back whole
+      uint64_t slot[kPerLane];
+      code_slots(codes[tile * NT + threadIdx.x], lo, slot);
+      const uint64_t vlo_b = lo * 4, vhi_b = (uint64_t)e.hi * 4, va0 = vlo_b & ~15ull;
+      char* lds = reinterpret_cast<char*>(sV);
+      stage_vals<NT>(lds, reinterpret_cast<const char*>(V), va0, vhi_b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      T* sv = reinterpret_cast<T*>(lds + (vlo_b - va0));
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        o[k] = (T)0.0f;
+        if (i0 + k < t1) {
+          o[k] = E::add1(sv[slot[k] - lo], v[k]);
+          sv[slot[k] - lo] = o[k];
+        }
+      }
+      __syncthreads();
+      const uint32_t nbytes = (uint32_t)(vhi_b - va0);
+      char* Vb = reinterpret_cast<char*>(V);
+      for (uint32_t c = threadIdx.x * 16u; c < nbytes; c += NT * 16u) {
+        const uint64_t gb = va0 + c;
+        if (gb >= vlo_b && c + 16u <= nbytes) {
+          *reinterpret_cast<u32x4*>(Vb + gb) = *reinterpret_cast<const u32x4*>(lds + c);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint64_t b = gb + 4u * j;
+            if (b >= vlo_b && b < vhi_b)
+              *reinterpret_cast<uint32_t*>(Vb + b) = *reinterpret_cast<const uint32_t*>(lds + c + 4u * j);
+          }
+        }
+      }
+      __syncthreads();  // the next tile stages into sV
+    }
+    if constexpr ((OP & PSG_PULL) != 0) {
+      if (whole && (vec & 1)) {
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]}),
+                                    reinterpret_cast<u32x4*>(outv + i0));
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k)
+          if (i0 + k < t1) outv[i0 + k] = o[k];
+      }
+    }
+  }
+  const uint64_t after = block_arrive(partial ? 2u : 0u, &s_cond, arrival);
+  request_done(after, arrival, uniform, rej + kPending, word, tag_bits, W_PARTIAL);
+}
+
 // __launch_bounds__(NT, 8): 8 waves per SIMD, i.e. two 1024-thread blocks per
 // CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
 // instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
@@ -801,6 +931,9 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
     if constexpr (MI && !CHECK) {
       const uint32_t tw = tword[tl];
       ne.pad = (tw >> 2) == (tile_tag(seq) >> 2) ? (tw & 3u) : kTileStretch;
+      // (vec bit 8: the follow-up of a k_tile_apply, which served every
+      // stretch and coded tile already: those run as tiles of no keys)
+      if ((vec & 8) && ne.pad != kTileGeneral) ne.pad = kTileDone;
       if (ne.pad == kTileCoded) ncode = codes[tl * NT + threadIdx.x];
     }
     if (ne.pad) {
@@ -841,11 +974,13 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
   if (blockIdx.x < ntiles) load_tile(blockIdx.x);
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * tileN;
-    const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
     // the window cached for this tile, staged speculatively: it is right when
     // it was computed against this K for this tile's first and last key
     // (checked below)
     const Win e = ne;
+    // (MI) a tile k_tile_apply served already runs as a stretch tile of no
+    // keys (uniform): nothing read or written, the next tile still prefetched
+    const uint64_t t1 = MI && e.pad == kTileDone ? t0 : ((t0 + tileN < n) ? t0 + tileN : n);
     const bool ident = MI && e.pad != 0;
     const bool cur = e.gen == gen;
     uint64_t lo = cur ? e.lo : 0, hi = cur ? e.hi : 0;
@@ -1770,6 +1905,7 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
     e->trusted = 0;
     e->strikes = 0;
     e->ident_fail = 0;
+    e->lean_fail = 0;
     e->ident_ok = 0;
     e->ident_trial = 0;
   }
@@ -1795,8 +1931,11 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
       if (s->chunk_ok) (void)hipFree(s->chunk_ok);
       s->chunk_ok = nullptr;
       s->chunk_cap = 0;
-      if (hipMalloc(&s->chunk_ok, cap * sizeof(int)) != hipSuccess) return nullptr;
-      if (hipMemsetAsync(s->chunk_ok, 0, cap * sizeof(int), st) != hipSuccess) return nullptr;
+      // one set per ring slot: a request's tile words stay its own while later
+      // requests in flight validate theirs (a follow-up of k_tile_apply reads
+      // them after those ran)
+      if (hipMalloc(&s->chunk_ok, (uint64_t)kRing * cap * sizeof(int)) != hipSuccess) return nullptr;
+      if (hipMemsetAsync(s->chunk_ok, 0, (uint64_t)kRing * cap * sizeof(int), st) != hipSuccess) return nullptr;
       s->chunk_cap = cap;
     }
   }
@@ -2024,6 +2163,12 @@ static uint32_t next_tag(psg_store* s) {
 
 static int drain(psg_store* s);
 
+// The tile words of the request validated in ring slot `ring`.
+static uint32_t* tile_words(psg_store* s, uint32_t ring) {
+  return reinterpret_cast<uint32_t*>(s->chunk_ok) + (uint64_t)ring * s->chunk_cap;
+}
+
+
 // Launch one fused request — k_validate_windows (skipped for a Pull on
 // trusted windows), then k_resolve_apply — and return without waiting.  Its
 // completion word arrives in ring slot rec->ring.
@@ -2045,14 +2190,14 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
     return e ? atoi(e) : 1;
   }();
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
-                  (aligned16(q) ? 2 : 0) | (vecw && aligned16(s->vals) ? 4 : 0);
+                  (aligned16(q) ? 2 : 0) | (vecw && aligned16(s->vals) ? 4 : 0) | (rec.lean == 2 ? 8 : 0);
   const unsigned g = grid_n(ntiles, 1);
   Arrival arr;
   arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
 #define PSG_RA_ARGS                                                                                     \
   q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end, (T*)s->vals, (const T*)vals, (T*)out, \
-      s->reject_dev, s->seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8,                           \
-      rec.mident ? (const uint32_t*)s->chunk_ok : nullptr, s->wc[rec.wc].codes
+      s->reject_dev, rec.seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8,                           \
+      rec.mident ? tile_words(s, rec.tw_ring) : nullptr, s->wc[rec.wc].codes
   // the 256-thread tiles of a request at most 2 in 5 of whose store's keys it
   // asks for stage windows of 4 tiles (32 KiB: 4 blocks per CU instead of 8)
   // — every 3rd key of the store: Push+Pull 333 -> 361 GB/s, every 4th 266 ->
@@ -2074,6 +2219,24 @@ static void launch_apply(psg_store* s, const uint64_t* q, uint64_t n, const void
   else
     k_resolve_apply<DT, OP, 256><<<g, 256, 0, st>>>(PSG_RA_ARGS);
 #undef PSG_RA_ARGS
+}
+
+// Launch k_tile_apply for a Push whose coded validation has run (launch_fused).
+template <int DT, int OP>
+static void launch_tile_apply(psg_store* s, uint64_t n, const void* vals, void* out, Win* win,
+                              const InflightReq& rec, hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  if constexpr (sizeof(T) == 4) {
+    const uint64_t ntiles = (n + 4095) / 4096;
+    const unsigned cus = (unsigned)(max_stream_blocks() / 8);
+    const unsigned g = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
+    const int vec = ((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0;
+    Arrival arr;
+    arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
+    k_tile_apply<DT, OP><<<g, 1024, 0, st>>>(n, win, (T*)s->vals, (const T*)vals, (T*)out, s->reject_dev, rec.seq,
+                                             vec, arr, s->ring_dev + rec.ring, rec.tag << 8, tile_words(s, rec.tw_ring),
+                                             s->wc[rec.wc].codes);
+  }
 }
 
 // PSG_RA_IDENT=0: never the identity kernels (A/B)
@@ -2153,6 +2316,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     wc->trusted = 0;
     wc->strikes = 0;
     wc->ident_fail = 0;
+    wc->lean_fail = 0;
     wc->ident_ok = 0;
   }
   Win* win = static_cast<Win*>(wc->win);
@@ -2202,17 +2366,19 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     (void)hipGetLastError();
     wc->codes = nullptr;
   }
-  if (mident && coded_on && wc->codes) {
+  const bool coded_ran = mident && coded_on && wc->codes;
+  if (coded_ran) {
     const unsigned cus = (unsigned)(max_stream_blocks() / 8);
     const unsigned gcode = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
     k_validate_code<<<gcode, 1024, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end,
-                                            s->reject_dev, seq, aligned16(q) ? 1 : 0, (uint32_t*)s->chunk_ok,
+                                            s->reject_dev, seq, aligned16(q) ? 1 : 0, tile_words(s, s->ring_next),
                                             wc->codes);
     s->counters[PSG_CTR_CODED]++;
   } else if (nsearch + nval > 0)
     k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
                                                          s->key_begin, s->key_end, s->reject_dev, seq,
-                                                         aligned16(q) ? 1 : 0, mident ? s->chunk_ok : nullptr);
+                                                         aligned16(q) ? 1 : 0,
+                                                         mident ? (int*)tile_words(s, s->ring_next) : nullptr);
   rec->ticket = ++s->next_ticket;
   if (ident && trial) wc->ident_trial = rec->ticket;
   rec->op = op;
@@ -2228,8 +2394,24 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   rec->ident = ident ? 1 : 0;
   rec->mident = mident ? 1 : 0;
   rec->nt = nt;
+  rec->seq = seq;
+  rec->tw_ring = rec->ring;  // (the slot the validation above wrote: ring_next then)
+  // the tiles the coded validation sorted as stretch or coded go to the lean
+  // apply (k_tile_apply) while this list's last attempt left no general tile
+  // against this K; f32 values (PSG_RA_LEAN=0: k_resolve_apply<MI>, A/B)
+  static const bool lean_on = [] {
+    const char* e = getenv("PSG_RA_LEAN");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const bool lean = lean_on && coded_ran && DT == PSG_F32 && (op & PSG_PUSH) && wc->lean_fail != s->gen;
+  rec->lean = lean ? 1 : 0;
   s->counters[ident ? PSG_CTR_IDENT : PSG_CTR_FUSED]++;
-  if (ident) {
+  if (lean) {
+    switch (op) {
+      case PSG_PUSH: launch_tile_apply<DT, PSG_PUSH>(s, n, vals, out, win, *rec, st); break;
+      default: launch_tile_apply<DT, PSG_PUSH | PSG_PULL>(s, n, vals, out, win, *rec, st); break;
+    }
+  } else if (ident) {
     switch (op) {
       case PSG_PUSH: launch_ident<DT, PSG_PUSH>(s, q, n, vals, out, win, *rec, st); break;
       case PSG_PULL: launch_ident<DT, PSG_PULL>(s, q, n, vals, out, win, *rec, st); break;
@@ -2341,6 +2523,36 @@ static int finish(psg_store* s, const InflightReq& r, uint32_t f) {
     InflightReq r2;
     PSG_TRY(launch_fused<DT>(s, r.op, r.q, r.n, r.vals, r.out, r.stream, &r2, r.want_land != 0));
     PSG_REQUIRE(!r2.ident, PSG_ERR_HIP, "SORTED store: identity request replayed as one");
+    s->inflight.push_back(r2);
+    int rc2 = PSG_OK;
+    const int rc = reap_t<DT>(s, r2.ticket, r2.ticket, &rc2);
+    return rc != PSG_OK ? rc : rc2;
+  }
+  if (f & W_PARTIAL) {
+    // k_tile_apply served the stretch and coded tiles and left the general
+    // ones: k_resolve_apply<MI> for the same request (same seq: it reads the
+    // tile words, skips the tiles marked done), to completion; no speculation
+    // on this list until K changes.  kPending, which the word raised, is
+    // cleared first so the follow-up is not gated.
+    if (wc.q == r.q && wc.n == r.n) wc.lean_fail = s->gen;
+    PSG_HIP(hipMemsetAsync(s->reject_dev + kPending, 0, sizeof(int), r.stream));
+    InflightReq r2 = r;
+    r2.ticket = ++s->next_ticket;
+    r2.ring = s->ring_next;
+    s->ring_next = (s->ring_next + 1) % kRing;
+    r2.tag = next_tag(s);
+    r2.lean = 2;  // (the follow-up: general tiles only)
+    r2.land = 0;
+    Win* win = static_cast<Win*>(wc.win);
+    switch (r.op) {
+      case PSG_PUSH: launch_apply<DT, PSG_PUSH>(s, r.q, r.n, r.vals, r.out, win, r2, r.stream); break;
+      default: launch_apply<DT, PSG_PUSH | PSG_PULL>(s, r.q, r.n, r.vals, r.out, win, r2, r.stream); break;
+    }
+    PSG_HIP(hipGetLastError());
+    if (r2.want_land && sync_poll() && s->land_ev[r2.ring]) {
+      PSG_HIP(hipEventRecord(s->land_ev[r2.ring], r.stream));
+      r2.land = 1;
+    }
     s->inflight.push_back(r2);
     int rc2 = PSG_OK;
     const int rc = reap_t<DT>(s, r2.ticket, r2.ticket, &rc2);

@@ -275,3 +275,52 @@ print("ok", st.counters()["coded"])
         assert last[0] == "ok"
         coded[env_val] = int(last[1])
     assert coded["0"] == 0 and coded["1"] >= 1, coded
+
+
+def test_partial_lean_apply_with_requests_in_flight_behind_it():
+    """The first lean apply (k_tile_apply) of a list whose seam tiles are
+    general leaves those to a follow-up (W_PARTIAL) that runs only when the
+    request is reaped — after the requests launched behind it have validated
+    their own tiles.  Each request keeps its own tile words (one set per ring
+    slot), so the follow-up applies exactly the seam tiles: a burst of requests
+    in flight right after the list's windows are trusted, bit-exact."""
+    dtype = psg.F32
+    rng, univ, st, orc = populated(dtype, 400000, 113)
+    # 16 stretches with 200 store keys left out at each seam; a 90 % subset
+    # in the middle
+    parts = [univ[j * 24000: j * 24000 + 23800] for j in range(16)]
+    parts[8] = subset(rng, parts[8], 0.9)
+    k = np.concatenate(parts)
+    dk = dev(k)
+    n = len(k)
+    request(st, orc, dtype, psg.PUSH, dk, k, 1)   # windows searched, then trusted
+    request(st, orc, dtype, psg.PUSH, dk, k, 2)   # the identity trial fails once
+    reqs, pending = [], []
+    for j in range(12):
+        flags = [psg.PUSH, psg.PUSH, ALL, psg.PULL][j % 4]
+        v = oracle.synth(n, dtype, 300 + j, 1, -1.0, 1.0)
+        dv = dev(v)
+        out = psg.DeviceBuffer(n * 4) if flags & psg.PULL else None
+        pending.append(st.handle_async(flags, dk, dv if flags & psg.PUSH else None, out, n))
+        reqs.append((dv, out, orc.handle(flags, k, v if flags & psg.PUSH else None, n)))
+    st.wait()
+    psg.device_sync()
+    for j, (_, out, exp) in enumerate(reqs):
+        if out is not None:
+            np.testing.assert_array_equal(out.download(np.float32, n), exp, err_msg=f"request {j}")
+    same_store(st, orc, dtype)
+    assert st.counters()["coded"] >= 1
+
+
+def test_lean_apply_with_many_tiles_per_block():
+    """A list of ~3 M keys (more tiles than the lean apply's blocks: each block
+    serves several) made of 12 stretches of the store: the first lean apply
+    serves the stretch tiles — every wave of a block on every tile — and
+    leaves the seam tiles to its follow-up; then requests in flight.  Found a
+    race (a block's first wave marking a tile done before its last wave read
+    the tile's kind) that under-applied whole waves: bit-exact now."""
+    dtype = psg.F32
+    rng, univ, st, orc = populated(dtype, 3300000, 127)
+    per = len(univ) // 12
+    k = np.concatenate([univ[j * per: (j + 1) * per - 300] for j in range(12)])
+    run_sequence(st, orc, dtype, k, 800)
