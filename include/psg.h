@@ -200,7 +200,12 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * the apply then reads no request keys and stages no window for a tile whose
  * keys are all in the store) */
 #define PSG_CTR_CODED 6
-#define PSG_NCOUNTERS 7
+/* of those, Pushes whose stretch and coded tiles went to the lean apply
+ * (k_tile_apply), and those of them that met a general tile and had it applied
+ * by a follow-up on the general path */
+#define PSG_CTR_LEAN 7
+#define PSG_CTR_LEAN_PARTIAL 8
+#define PSG_NCOUNTERS 9
 int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):

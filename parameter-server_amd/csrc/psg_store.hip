@@ -2407,6 +2407,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   rec->lean = lean ? 1 : 0;
   s->counters[ident ? PSG_CTR_IDENT : PSG_CTR_FUSED]++;
   if (lean) {
+    s->counters[PSG_CTR_LEAN]++;
     switch (op) {
       case PSG_PUSH: launch_tile_apply<DT, PSG_PUSH>(s, n, vals, out, win, *rec, st); break;
       default: launch_tile_apply<DT, PSG_PUSH | PSG_PULL>(s, n, vals, out, win, *rec, st); break;
@@ -2531,9 +2532,10 @@ static int finish(psg_store* s, const InflightReq& r, uint32_t f) {
   if (f & W_PARTIAL) {
     // k_tile_apply served the stretch and coded tiles and left the general
     // ones: k_resolve_apply<MI> for the same request (same seq: it reads the
-    // tile words, skips the tiles marked done), to completion; no speculation
-    // on this list until K changes.  kPending, which the word raised, is
-    // cleared first so the follow-up is not gated.
+    // request's tile words and takes every tile not general as done), to
+    // completion; no speculation on this list until K changes.  kPending,
+    // which the word raised, is cleared first so the follow-up is not gated.
+    s->counters[PSG_CTR_LEAN_PARTIAL]++;
     if (wc.q == r.q && wc.n == r.n) wc.lean_fail = s->gen;
     PSG_HIP(hipMemsetAsync(s->reject_dev + kPending, 0, sizeof(int), r.stream));
     InflightReq r2 = r;

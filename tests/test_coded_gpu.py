@@ -309,14 +309,18 @@ def test_partial_lean_apply_with_requests_in_flight_behind_it():
         if out is not None:
             np.testing.assert_array_equal(out.download(np.float32, n), exp, err_msg=f"request {j}")
     same_store(st, orc, dtype)
-    assert st.counters()["coded"] >= 1
+    c = st.counters()
+    assert c["coded"] >= 1
+    # the Pushes after the trial went lean; the first met the seam tiles
+    assert c["lean"] >= 1 and c["lean_partial"] >= 1, c
 
 
 def test_lean_apply_with_many_tiles_per_block():
     """A list of ~3 M keys (more tiles than the lean apply's blocks: each block
-    serves several) made of 12 stretches of the store: the first lean apply
-    serves the stretch tiles — every wave of a block on every tile — and
-    leaves the seam tiles to its follow-up; then requests in flight.  Found a
+    serves several) made of 12 stretches of the store, 300 store keys left out
+    at each seam (a seam tile's window spans both sides: coded), so every
+    Push after the trial is lean — every wave of a block on every tile; then
+    requests in flight.  Found a
     race (a block's first wave marking a tile done before its last wave read
     the tile's kind) that under-applied whole waves: bit-exact now."""
     dtype = psg.F32
@@ -324,3 +328,5 @@ def test_lean_apply_with_many_tiles_per_block():
     per = len(univ) // 12
     k = np.concatenate([univ[j * per: (j + 1) * per - 300] for j in range(12)])
     run_sequence(st, orc, dtype, k, 800)
+    c = st.counters()
+    assert c["lean"] >= 1 and c["lean_partial"] == 0, c

@@ -192,3 +192,8 @@ def test_keyed_bench_line_store_layouts(env_extra, coded):
     assert (paths["coded"] > 0) == coded, paths
     kernel = line["roofline"]["kernel"]
     assert ("k_validate_code" in kernel) == coded, kernel
+    # f32 Pushes of coded lists go to the lean apply (k_tile_apply) — except
+    # where the general tiles keep sending them back (the store's own list
+    # under PSG_RA_IDENT=0 has none: lean too)
+    if coded:
+        assert paths["lean"] > 0 and "k_tile_apply" in kernel, (paths, kernel)
