@@ -1026,12 +1026,13 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "in flight, each reporting completion and flags in one "
                      "kernel-written word; one server, so no slicer pass)")
         elif 2 * paths.get("lean", 0) > paths["coded"]:  # most coded Pushes went lean
-            kname = ("SORTED-store Push: k_validate_code + k_tile_apply "
+            kname = ("SORTED-store Push: k_validate_code + k_tile_apply_db "
                      "(whole-request validation before any write, which also sorts the "
                      "tiles on trusted windows; the lean apply then takes stretches of "
                      "the store at slots lo + i and subsets of their window at places "
                      "from lane codes cached with the windows and verified each request "
-                     "— no key re-read, no search; a general tile, if one appears, is "
+                     "(a coded tile's window staged into LDS while the block's previous "
+                     "tile is applied) — no key re-read, no search; a general tile, if one appears, is "
                      "applied by a k_resolve_apply follow-up and the list goes back to "
                      "it until the store's keys change; requests in flight, each "
                      "reporting completion and flags in one kernel-written word; one "

@@ -860,6 +860,215 @@ __global__ __launch_bounds__(1024, 8) void k_tile_apply(uint64_t n, const Win* _
   request_done(after, arrival, uniform, rej + kPending, word, tag_bits, W_PARTIAL);
 }
 
+// The whole 16-B chunks of a coded tile's values (stage_vals' DMA half), issued
+// a tile ahead by k_tile_apply_db.
+template <int NT>
+__device__ __forceinline__ void stage_chunks(char* lds, const char* V, uint64_t va0, uint64_t vhi_b) {
+  const uint32_t nfull = (uint32_t)((vhi_b - va0) & ~15ull);
+  const char* src = V + va0;
+  for (uint32_t c = (threadIdx.x >> 6) * 1024u; c < nfull; c += (NT / 64) * 1024u) {
+    const uint32_t off = c + (threadIdx.x & 63) * 16u;
+    if (off < nfull)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + off),
+                                       (__attribute__((address_space(3))) void*)(lds + c), 16, 0, 0);
+  }
+}
+
+// A block barrier for LDS alone: this wave's LDS accesses done, then the
+// barrier — without __syncthreads()'s fence, which would also wait for every
+// global access in flight (the next tile's staging among them)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+constexpr uint32_t kTaBuf = 2 * 1024 * kPerLane * 4 + 32;  // bytes: a window of at most 8192 values + alignment
+__shared__ __attribute__((aligned(16))) char ta_buf0[kTaBuf];
+__shared__ __attribute__((aligned(16))) char ta_buf1[kTaBuf];
+
+// One tile of k_tile_apply_db, its window (if coded) in ta_buf<B>, staging the
+// block's next tile into the other buffer meanwhile.
+template <int DT, int OP, int B>
+__device__ __forceinline__ void tile_apply_step(uint64_t tile, uint64_t n, uint64_t ntiles, const Win* __restrict__ win,
+                                                typename Elem<DT>::T* __restrict__ V,
+                                                const typename Elem<DT>::T* __restrict__ vals,
+                                                typename Elem<DT>::T* __restrict__ outv, int vec, uint32_t tag,
+                                                const uint32_t* __restrict__ tword,
+                                                const uint32_t* __restrict__ codes, int& partial) {
+  using E = Elem<DT>;
+  using T = typename E::T;
+  constexpr int NT = 1024;
+  constexpr uint64_t tileN = (uint64_t)NT * kPerLane;
+  char* const lds = B ? ta_buf1 : ta_buf0;
+  char* const other = B ? ta_buf0 : ta_buf1;
+  const char* Vc = reinterpret_cast<const char*>(V);
+  auto kind = [&](uint64_t t) -> uint32_t {
+    const uint32_t tw = tword[t];
+    return (tw >> 2) == (tag >> 2) ? (tw & 3u) : (uint32_t)kTileGeneral;
+  };
+  const uint64_t next = tile + gridDim.x;
+  const bool next_coded = next < ntiles && kind(next) == kTileCoded;
+  auto stage_next = [&]() {
+    if (next_coded) {
+      const Win e2 = win[next];
+      stage_chunks<NT>(other, Vc, ((uint64_t)e2.lo * 4) & ~15ull, (uint64_t)e2.hi * 4);
+    }
+  };
+  const uint32_t st = kind(tile);
+  if (st != kTileStretch && st != kTileCoded) {  // (uniform) the follow-up's
+    partial = 1;
+    stage_next();
+    return;
+  }
+  const uint64_t t0 = tile * tileN;
+  const uint64_t t1 = (t0 + tileN < n) ? t0 + tileN : n;
+  const uint64_t i0 = t0 + (uint64_t)threadIdx.x * kPerLane;
+  const Win e = win[tile];
+  const uint64_t lo = e.lo;
+  const bool whole = i0 + kPerLane <= t1;
+  T v[kPerLane];
+  if (whole && (vec & 1)) {
+    const f32x4 x = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + i0)));
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) v[k] = i0 + k < t1 ? vals[i0 + k] : (T)0.0f;
+  }
+  T o[kPerLane];
+  if (st == kTileStretch) {
+    // done in registers before the next tile's staging is issued (a load
+    // after it would wait for it)
+    const uint64_t s0 = lo + (i0 - t0);
+    if (whole && (s0 & 3) == 0) {
+      f32x4 x = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(V + s0));
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        o[k] = E::add1(x[k], v[k]);
+        x[k] = o[k];
+      }
+      *reinterpret_cast<u32x4*>(V + s0) = __builtin_bit_cast(u32x4, x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) {
+        o[k] = (T)0.0f;
+        if (i0 + k < t1) {
+          o[k] = E::add1(V[s0 + k], v[k]);
+          V[s0 + k] = o[k];
+        }
+      }
+    }
+    stage_next();
+  } else {
+    // this tile's code, values and last partial chunk, all landed (with the
+    // chunks staged a round ago, issued before them) before the next tile's
+    // staging goes out
+    const uint64_t vlo_b = lo * 4, vhi_b = (uint64_t)e.hi * 4, va0 = vlo_b & ~15ull;
+    const uint32_t nfull = (uint32_t)((vhi_b - va0) & ~15ull);
+    const uint32_t tail = (uint32_t)(vhi_b - va0) - nfull;
+    const uint32_t code = codes[tile * NT + threadIdx.x];
+    uint32_t tailv = 0;
+    if (threadIdx.x * 4u < tail) tailv = *reinterpret_cast<const uint32_t*>(Vc + va0 + nfull + threadIdx.x * 4u);
+    asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(code), "v"(tailv));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stage_next();
+    uint64_t slot[kPerLane];
+    code_slots(code, lo, slot);
+    if (threadIdx.x * 4u < tail) *reinterpret_cast<uint32_t*>(lds + nfull + threadIdx.x * 4u) = tailv;
+    lds_barrier();
+    T* sv = reinterpret_cast<T*>(lds + (vlo_b - va0));
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      o[k] = (T)0.0f;
+      if (i0 + k < t1) {
+        o[k] = E::add1(sv[slot[k] - lo], v[k]);
+        sv[slot[k] - lo] = o[k];
+      }
+    }
+    lds_barrier();
+    const uint32_t nbytes = (uint32_t)(vhi_b - va0);
+    char* Vb = reinterpret_cast<char*>(V);
+    for (uint32_t c = threadIdx.x * 16u; c < nbytes; c += NT * 16u) {
+      const uint64_t gb = va0 + c;
+      if (gb >= vlo_b && c + 16u <= nbytes) {
+        *reinterpret_cast<u32x4*>(Vb + gb) = *reinterpret_cast<const u32x4*>(lds + c);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint64_t bb = gb + 4u * j;
+          if (bb >= vlo_b && bb < vhi_b)
+            *reinterpret_cast<uint32_t*>(Vb + bb) = *reinterpret_cast<const uint32_t*>(lds + c + 4u * j);
+        }
+      }
+    }
+    lds_barrier();  // this buffer read out before the round after next stages into it
+  }
+  if constexpr ((OP & PSG_PULL) != 0) {
+    if (whole && (vec & 1)) {
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]}),
+                                  reinterpret_cast<u32x4*>(outv + i0));
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k)
+        if (i0 + k < t1) outv[i0 + k] = o[k];
+    }
+  }
+}
+
+// k_tile_apply with the coded tiles' values staged a tile ahead: while a block
+// updates and writes back tile t's stretch of values from one LDS buffer, the
+// DMA of its next tile's (t + grid) fills the other — a block keeps two
+// windows in flight instead of one (128 KiB of LDS per CU at two blocks).
+// Tile windows are disjoint (k_validate_code's exactness: a coded tile's
+// first key at place 0, its last at W - 1), so staging the next before this
+// one is written back reads no value this kernel writes — but for the up to
+// 3 values before lo that the 16-B alignment stages and the write-back skips.
+// The last partial chunk (at most 3 values) is read through VGPRs in the
+// tile's own round, as stage_vals does.  The block's tiles alternate between
+// the two buffers (two static arrays: the compiler sees that the LDS accesses
+// of one tile cannot alias the other's staging, and waits for nothing of it).
+// (PSG_TA_DB=0: k_tile_apply, A/B.)
+template <int DT, int OP>
+__global__ __launch_bounds__(1024, 8) void k_tile_apply_db(uint64_t n, const Win* __restrict__ win,
+                                                           typename Elem<DT>::T* __restrict__ V,
+                                                           const typename Elem<DT>::T* __restrict__ vals,
+                                                           typename Elem<DT>::T* __restrict__ outv,
+                                                           int* __restrict__ rej, int seq, int vec, Arrival arrival,
+                                                           uint32_t* __restrict__ word, uint32_t tag_bits,
+                                                           const uint32_t* __restrict__ tword,
+                                                           const uint32_t* __restrict__ codes) {
+  static_assert(sizeof(typename Elem<DT>::T) == 4, "4-byte values");
+  constexpr uint64_t tileN = 1024 * kPerLane;
+  __shared__ uint32_t s_cond;
+  if (threadIdx.x == 0) s_cond = 0;
+  __syncthreads();
+  uint32_t uniform = rej[kPending] != 0 ? (uint32_t)W_GATED : 0u;
+  if (rej[kRejRange] == seq) uniform |= W_RANGE;
+  if (rej[kRejUnsorted] == seq) uniform |= W_UNSORTED;
+  const uint64_t ntiles = uniform ? 0 : (n + tileN - 1) / tileN;
+  const uint32_t tag = tile_tag(seq);
+  // the first tile's chunks
+  if (blockIdx.x < ntiles) {
+    const uint32_t tw = tword[blockIdx.x];
+    if ((tw >> 2) == (tag >> 2) && (tw & 3u) == kTileCoded) {
+      const Win e = win[blockIdx.x];
+      stage_chunks<1024>(ta_buf0, reinterpret_cast<const char*>(V), ((uint64_t)e.lo * 4) & ~15ull,
+                         (uint64_t)e.hi * 4);
+    }
+  }
+  int partial = 0;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += 2 * (uint64_t)gridDim.x) {
+    tile_apply_step<DT, OP, 0>(tile, n, ntiles, win, V, vals, outv, vec, tag, tword, codes, partial);
+    if (tile + gridDim.x < ntiles)
+      tile_apply_step<DT, OP, 1>(tile + gridDim.x, n, ntiles, win, V, vals, outv, vec, tag, tword, codes, partial);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no staging left in flight)
+  __syncthreads();
+  const uint64_t after = block_arrive(partial ? 2u : 0u, &s_cond, arrival);
+  request_done(after, arrival, uniform, rej + kPending, word, tag_bits, W_PARTIAL);
+}
+
 // __launch_bounds__(NT, 8): 8 waves per SIMD, i.e. two 1024-thread blocks per
 // CU (the LDS holds two 64 KiB windows).  Without the bound the Pull
 // instantiation used 91 SGPRs (97 with VCC and the rest): one block per CU,
@@ -2233,9 +2442,18 @@ static void launch_tile_apply(psg_store* s, uint64_t n, const void* vals, void* 
     const int vec = ((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0;
     Arrival arr;
     arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
-    k_tile_apply<DT, OP><<<g, 1024, 0, st>>>(n, win, (T*)s->vals, (const T*)vals, (T*)out, s->reject_dev, rec.seq,
-                                             vec, arr, s->ring_dev + rec.ring, rec.tag << 8, tile_words(s, rec.tw_ring),
-                                             s->wc[rec.wc].codes);
+    static const bool db = [] {
+      const char* e = getenv("PSG_TA_DB");
+      return e ? atoi(e) != 0 : true;
+    }();
+    if (db)
+      k_tile_apply_db<DT, OP><<<g, 1024, 0, st>>>(n, win, (T*)s->vals, (const T*)vals, (T*)out, s->reject_dev,
+                                                  rec.seq, vec, arr, s->ring_dev + rec.ring, rec.tag << 8,
+                                                  tile_words(s, rec.tw_ring), s->wc[rec.wc].codes);
+    else
+      k_tile_apply<DT, OP><<<g, 1024, 0, st>>>(n, win, (T*)s->vals, (const T*)vals, (T*)out, s->reject_dev, rec.seq,
+                                               vec, arr, s->ring_dev + rec.ring, rec.tag << 8,
+                                               tile_words(s, rec.tw_ring), s->wc[rec.wc].codes);
   }
 }
 
