@@ -1,7 +1,8 @@
 """Coded tiles on the SORTED store (csrc/psg_store.hip, k_validate_code): a Push
 on trusted windows whose tiles are subsets of their windows is resolved in its
-validation pass, and k_resolve_apply serves those tiles from the lane codes —
-no request key re-read, no window, no search.  A list that is a random subset
+validation pass, and the lean apply (k_tile_apply_db; f32) or k_resolve_apply
+serves those tiles from the lane codes — no request key re-read, no window,
+no search; a general tile met by the lean apply is applied by a follow-up.  A list that is a random subset
 of the store's keys takes that path; tiles with absent
 keys, with keys too far apart for a code, or with windows wider than 8192 keys
 take the general path in the same request.  Every case is bit-exact against
@@ -139,7 +140,11 @@ def test_coded_tiles_beside_absent_keys_and_wide_gaps():
     k = np.unique(np.concatenate([k, fresh, univ[396000:396000 + 3001]]))
     assert len(univ) < 1.5 * len(k)
     run_sequence(st, orc, dtype, k, 900)
-    assert st.counters()["coded"] >= 4
+    c = st.counters()
+    assert c["coded"] >= 4, c
+    # the first lean apply met the general tiles: a follow-up, then the list
+    # stays on k_resolve_apply
+    assert c["lean"] >= 1 and c["lean_partial"] >= 1, c
     # new absent keys in a list whose other keys were coded
     more = np.setdiff1d(univ[5:100000:13] + np.uint64(3), univ)
     k2 = np.unique(np.concatenate([k, more]))
@@ -156,7 +161,8 @@ def test_coded_tiles_ragged_sizes(n_keys):
     k = np.sort(rng.choice(univ, n_keys, replace=False))
     run_sequence(st, orc, dtype, k, 40 + n_keys, inflight=n_keys > 3)
     if n_keys >= 4095:
-        assert st.counters()["coded"] >= 1
+        c = st.counters()
+        assert c["coded"] >= 1 and c["lean"] >= 1, c
 
 
 def test_coded_list_rewritten_shifted_under_the_same_pointer():
@@ -328,5 +334,18 @@ def test_lean_apply_with_many_tiles_per_block():
     per = len(univ) // 12
     k = np.concatenate([univ[j * per: (j + 1) * per - 300] for j in range(12)])
     run_sequence(st, orc, dtype, k, 800)
+    c = st.counters()
+    assert c["lean"] >= 1 and c["lean_partial"] == 0, c
+
+
+def test_lean_apply_coded_tiles_many_per_block():
+    """A random 90 % subset of a 3.3 M-key store (~730 coded tiles, more than
+    the lean apply's blocks): a block stages its next coded tile's window into
+    its second LDS buffer while it applies the current one — Pushes, PushPulls
+    and Pulls, then in flight, bit-exact."""
+    dtype = psg.F32
+    rng, univ, st, orc = populated(dtype, 3300000, 131)
+    k = subset(rng, univ, 0.9)
+    run_sequence(st, orc, dtype, k, 1700)
     c = st.counters()
     assert c["lean"] >= 1 and c["lean_partial"] == 0, c
