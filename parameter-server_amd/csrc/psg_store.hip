@@ -2438,7 +2438,12 @@ static void launch_tile_apply(psg_store* s, uint64_t n, const void* vals, void* 
   if constexpr (sizeof(T) == 4) {
     const uint64_t ntiles = (n + 4095) / 4096;
     const unsigned cus = (unsigned)(max_stream_blocks() / 8);
-    const unsigned g = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
+    // PSG_TA_BPC (A/B): blocks per CU in the grid (0: one block per tile)
+    static const int ta_bpc = [] {
+      const char* e = getenv("PSG_TA_BPC");
+      return e ? atoi(e) : 2;
+    }();
+    const unsigned g = (unsigned)(ta_bpc > 0 ? std::min<uint64_t>(ntiles, (uint64_t)cus * ta_bpc) : ntiles);
     const int vec = ((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0;
     Arrival arr;
     arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
@@ -2587,7 +2592,12 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   const bool coded_ran = mident && coded_on && wc->codes;
   if (coded_ran) {
     const unsigned cus = (unsigned)(max_stream_blocks() / 8);
-    const unsigned gcode = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
+    // PSG_VC_BPC (A/B): blocks per CU in the grid (0: one block per tile)
+    static const int vc_bpc = [] {
+      const char* e = getenv("PSG_VC_BPC");
+      return e ? atoi(e) : 2;
+    }();
+    const unsigned gcode = (unsigned)(vc_bpc > 0 ? std::min<uint64_t>(ntiles, (uint64_t)cus * vc_bpc) : ntiles);
     k_validate_code<<<gcode, 1024, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end,
                                             s->reject_dev, seq, aligned16(q) ? 1 : 0, tile_words(s, s->ring_next),
                                             wc->codes);
