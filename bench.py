@@ -1033,8 +1033,8 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "from lane codes cached with the windows and verified each request "
                      "(a coded tile's window staged into LDS while the block's previous "
                      "tile is applied) — no key re-read, no search; a general tile, if one appears, is "
-                     "applied by a k_resolve_apply follow-up and the list goes back to "
-                     "it until the store's keys change; requests in flight, each "
+                     "applied by a follow-up on the general path and the list stays "
+                     "there until the store's keys change; requests in flight, each "
                      "reporting completion and flags in one kernel-written word; one "
                      "server, so no slicer pass)")
         else:

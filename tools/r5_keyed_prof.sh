@@ -15,7 +15,7 @@ import csv, glob, sys
 for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Name"]
-        if any(k in n for k in ("k_validate", "k_resolve_apply", "k_ident", "k_dense_vec")):
+        if any(k in n for k in ("k_validate", "k_resolve_apply", "k_tile_apply", "k_ident", "k_dense_vec")):
             print(f"  {n[:90]:90s} calls {r['Calls']:>5s} avg {float(r['AverageNs'])/1e3:8.2f} us")
 PY
 done
