@@ -34,6 +34,7 @@ import argparse
 import json
 import os
 import platform
+import socket
 import sys
 import time
 
@@ -100,7 +101,27 @@ class GpuBackend:
         # round-robin, and RCCL — which refuses two ranks on one GPU — is not
         # used, so the xGMI exchange path of N > 1 can run on a 1-GPU box.
         self.share_gpu = os.environ.get("PSG_BENCH_SHARE_GPU") == "1"
-        psg.set_device(local_rank % psg.device_count() if self.share_gpu else local_rank)
+        ndev = psg.device_count()
+        if world > 1 and not self.share_gpu and local_rank >= ndev:
+            raise SystemExit(f"bench.py rank {rank}: LOCAL_RANK {local_rank} but {ndev} GPU(s) visible; one GPU per "
+                             "rank is required (PSG_BENCH_SHARE_GPU=1: the shared-GPU test mode)")
+        self.device = local_rank % ndev if self.share_gpu else local_rank
+        psg.set_device(self.device)
+        self.pci_bus_id = psg.device_pci_bus_id(self.device)
+        self.host = socket.gethostname()
+        if world > 1 and not self.share_gpu:
+            # one GPU per rank, or the line would measure ranks sharing a device
+            # (VERDICT r5 next #5): every rank names its physical GPU, and a
+            # duplicate ends the job on every rank before RCCL starts
+            seen = group.all_gather((self.host, self.pci_bus_id, rank))
+            where = {}
+            for h, pci, r in seen:
+                where.setdefault((h, pci), []).append(r)
+            dup = {k: v for k, v in where.items() if len(v) > 1}
+            if dup:
+                (h, pci), rs = next(iter(dup.items()))
+                raise SystemExit(f"bench.py: ranks {rs} all run on GPU {pci} of {h}; one GPU per rank is "
+                                 "required (PSG_BENCH_SHARE_GPU=1: the shared-GPU test mode)")
         self.stream = psg.Stream()
         self.comm = None
         self.xgmi = None
@@ -109,6 +130,16 @@ class GpuBackend:
         self.fused = False
         self.nbuckets = 1
         self.max_pushes = 1 << 10
+
+    def describe(self) -> dict:
+        """Where this rank ran: its HIP device, that GPU's PCI bus id and host,
+        and the rank / rank count RCCL reports (psg_comm_rank) when it is up."""
+        d = {"rank": self.rank, "device": self.device, "pci_bus_id": self.pci_bus_id, "host": self.host}
+        if self.comm is not None:
+            d["rccl_rank"], d["rccl_nranks"] = self.comm.rank()
+        else:
+            d["rccl_rank"] = d["rccl_nranks"] = None
+        return d
 
     def setup(self, L: int, seed: int):
         p = self.p
@@ -891,6 +922,8 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         if not isinstance(chk, dict):
             chk = {"ok": bool(chk)}
     acc_ms = backend.accumulate_probe() if (world > 1 and hasattr(backend, "accumulate_probe")) else None
+    # every rank's device, GPU and RCCL view, gathered for the line (N > 1)
+    ranks = group.all_gather(backend.describe()) if (world > 1 and hasattr(backend, "describe")) else None
     ms, push_ms, pull_ms, acc = group.allreduce_max([local_ms, push_ms, pull_ms, acc_ms or 0.0])
     acc_ms = acc if acc_ms is not None else None
     ok = None
@@ -970,6 +1003,12 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
             res["config"]["xgmi_checksum_verified"] = backend.exchange_verified
         if getattr(backend, "share_gpu", False):
             res["config"]["shared_gpu_test_mode"] = True
+    if ranks is not None:
+        # which device, GPU (PCI bus id, host) and RCCL rank each rank had, and
+        # the exchange calibration: the first N-GPU line proves its own layout
+        res["config"]["ranks"] = ranks
+        res["config"]["distinct_gpus"] = len({(d.get("host"), d.get("pci_bus_id")) for d in ranks})
+        res["config"].setdefault("calibration_ms", getattr(backend, "calibration", None))
     if world == 1 and getattr(backend, "cached", False) and getattr(backend, "stretch", None) is not None:
         # the cached list resolved to a stretch of slots: no slot stream, so the
         # request's bytes are those of the dense op on that stretch
@@ -1226,6 +1265,7 @@ def run_dropin(args, n_gpus: int) -> dict:
         raise SystemExit(f"kv_bench_dropin failed ({r.returncode}): {r.stderr[-2000:]}")
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     workers = [l for l in lines if "rank" in l]
+    servers = [l for l in lines if "server" in l]
     if len(workers) != N:
         raise SystemExit(f"kv_bench_dropin: {len(workers)} worker lines for {N} workers")
     ms = max(w["ms_per_step"] for w in workers)
@@ -1260,6 +1300,14 @@ def run_dropin(args, n_gpus: int) -> dict:
         "roofline": roof,
         "job_wall_s": round(wall, 2),
     }
+    if servers:
+        # how the servers' stores served the job's requests (psg_store_counters):
+        # runs in one pass (same list / strided) and the requests they held,
+        # of N * N * 2 * (warmup + steps) requests in all
+        tot = {k: sum(sv.get(k, 0) for sv in servers) for k in
+               ("fused", "ident", "runs", "run_frames", "strided_runs", "strided_frames")}
+        tot["requests"] = N * N * 2 * (args.warmup + args.steps)
+        res["server_counters"] = tot
     if not args.no_cpu_baseline:
         import oracle
         t0 = time.perf_counter()

@@ -93,6 +93,11 @@ int psg_device_count(int* n);
 /* Bind the calling thread to a GPU (hipSetDevice). */
 int psg_set_device(int device);
 int psg_get_device(int* device);
+/* The PCI bus id of `device` ("0000:05:00.0", hipDeviceGetPCIBusId) into buf
+ * (len bytes, NUL-terminated).  No reference counterpart: a multi-GPU job
+ * records which physical GPU each rank ran on (bench.py), and refuses two
+ * ranks on one GPU. */
+int psg_device_pci_bus_id(int device, char* buf, int len);
 int psg_device_sync(void);
 /* Let kernels on `device` read/write `peer`'s HBM over xGMI (idempotent). */
 int psg_enable_peer_access(int device, int peer);
@@ -205,7 +210,11 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * by a follow-up on the general path */
 #define PSG_CTR_LEAN 7
 #define PSG_CTR_LEAN_PARTIAL 8
-#define PSG_NCOUNTERS 9
+/* runs of queued requests on interleaved key lists served in one pass
+ * (psg_store_run, PSG_RUN_STRIDED), and the requests those runs held */
+#define PSG_CTR_STRIDED_RUNS 9
+#define PSG_CTR_STRIDED_FRAMES 10
+#define PSG_NCOUNTERS 11
 int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):
@@ -289,6 +298,42 @@ int psg_store_wait(psg_store* s, uint64_t ticket);
 int psg_store_push_frames(psg_store* s, const uint64_t* const* keys_host, uint64_t first_key,
                           const void* const* vals_host, int k, uint64_t n, psg_stream stream,
                           int* fused_host);
+
+/* A run of k requests queued one behind the other at a server — Pushes, Pulls
+ * and PushPulls, each on its own key list — served with the result of
+ *     for j < k:  psg_store_handle(s, ops[j], keys[j], 0, vals[j], outs[j],
+ *                                  ns[j], stream)
+ * (the reference's receive thread takes queued messages one at a time,
+ * src/internal/Customer.cpp:52-70, and serves each with its own loop,
+ * src/ps/KVApp.h:446-454).  Two layouts are served in one pass:
+ *   PSG_RUN_SAME_LIST  every request a Push on one list (nw workers of a BSP
+ *                      round): as psg_store_push_frames, each key's values
+ *                      added in order j = 0, 1, ...;
+ *   PSG_RUN_STRIDED    the lists are distinct phases of one period P <= 64 of
+ *                      the store's keys, keys[j][i] == K[D + p_j + P i] — the
+ *                      reference benchmark's layout `kMaxKey / num * i + rank`
+ *                      (tests/test_kv_app_benchmark.cpp:47-52) at nw workers,
+ *                      P = nw.  Such lists are pairwise disjoint: every store
+ *                      value is touched by at most one request, so the order
+ *                      of the run changes no result, and one pass over the
+ *                      slots they span serves them: 28 B per pushed and 24 per
+ *                      pulled f32 key (request and store keys 16, values),
+ *                      against 8 P + 8 P of store lines per key for each
+ *                      request on its own.
+ * Any other run — lists that overlap or differ in layout, absent keys, keys out
+ * of order — is served request by request, exactly as the k calls (a request
+ * that fails stops the run there and returns its status).  Every key is
+ * checked before any value is written: a run a pass rejects leaves the store
+ * as it found it.  keys[j], vals[j] (Push), outs[j] (Pull): device arrays of
+ * ns[j] elements; 1 <= k <= 16.  *served (may be NULL) = PSG_RUN_*.  Returns
+ * as psg_store_handle does: every key and value array is no longer read and
+ * every Pull's reply is in memory.  PSG_RUNS_STRIDED=0 never tries the
+ * strided pass (A/B). */
+#define PSG_RUN_ONE_BY_ONE 0
+#define PSG_RUN_SAME_LIST 1
+#define PSG_RUN_STRIDED 2
+int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
+                  const void* const* vals, void* const* outs, psg_stream stream, int* served);
 
 /* The stable device radix sort of the order-preserving path (psg_sort.hip),
  * exported for its parity tests: sorts (keys[i], vals[i]) by bits [0, bits) of

@@ -183,6 +183,7 @@ struct InflightReq {
   int lean;       // applied by k_tile_apply (its stretch and coded tiles; general ones follow up)
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
+struct RunSeen;            // psg_runs.hip (below)
 }  // namespace psg
 
 struct psg_store {
@@ -259,6 +260,24 @@ struct psg_store {
   // stretch / coded / general for the request that wrote it
   int* chunk_ok;      // per ring slot, per tile: the tile words of the request in that slot (psg_store.hip)
   uint64_t chunk_cap;  // tiles per ring slot
+  // the layout of the current run of queued requests (psg_runs.hip, device
+  // psg::RunDesc), and how the last runs went (psg_store_run)
+  void* run_desc;
+  psg::RunSeen* run_seen;  // pinned host: what the last classify saw
+  // list positions learnt from strided runs: a list (device pointer, n) whose
+  // first key sat at slot pos0 of K generation gen, in a layout of period P
+  struct RunPos {
+    const uint64_t* q;
+    uint64_t n;
+    uint64_t pos0;
+    uint32_t P;
+    uint32_t gen;
+    uint64_t last_use;
+  } run_pos[64];
+  uint64_t run_clock;
+  int run_last;       // PSG_RUN_* the last run was served as
+  uint32_t run_fail_gen;  // K's generation at which a run with Pulls was not strided
+  int run_fail_count;     // ... and how many runs since were served one by one without trying
 };
 
 struct psg_adam {
@@ -309,6 +328,56 @@ int frames_apply(int dtype, void* store_vals, uint64_t store_elems, const void* 
                  const uint64_t* base, const int* rej, int seq, int* flag, hipStream_t st);
 int frames_slots(int dtype, void* store_vals, const uint32_t* slots, const void* const* vals, int k, uint64_t n,
                  const int* rej, int seq, int* flag, hipStream_t st);
+// A run of queued requests on interleaved key lists (psg_runs.hip): request j
+// holds every P-th key of the store from its own phase,
+//     keys_j[i] == K[D + p_j + P * i]   for i < n_j,
+// with the phases p_j distinct — so the lists are pairwise disjoint, every
+// store slot is touched by at most one request, and the requests commute: one
+// pass over the slots [D, D + span) serves them all with the result of the
+// queued sequence.  That is the reference benchmark's key layout
+// (tests/test_kv_app_benchmark.cpp:47-52, `kMaxKey / num * i + rank`) at
+// nw workers: each server's store holds the nw lists interleaved, P = nw.
+constexpr int kRunMaxPeriod = 64;
+enum { RUN_NONE = 0, RUN_SAME = 1, RUN_STRIDED = 2 };
+struct RunDesc {
+  uint64_t D;     // the store slot of the run's lowest first key
+  uint64_t rows;  // rows [0, rows): slots D + P * row + phase
+  uint32_t P;     // period
+  int cls;        // RUN_*: what run_classify found (from first keys only)
+  int8_t map[kRunMaxPeriod];  // phase -> request, -1: a phase no request holds
+};
+// what run_classify saw, mirrored to pinned host memory for the host's cache
+// of list positions (psg_store_run): the slot of each list's first key
+struct RunSeen {
+  RunDesc d;
+  uint64_t pos[16];
+  int found[16];
+};
+struct RunFrames {
+  const uint64_t* q[kMaxFrames];  // keys of request j (device)
+  const void* v[kMaxFrames];      // its pushed values (PSG_PUSH)
+  void* o[kMaxFrames];            // its reply values (PSG_PULL)
+  uint64_t n[kMaxFrames];         // its keys
+  int op[kMaxFrames];             // PSG_PUSH | PSG_PULL bits
+};
+// run_classify: one block; from the requests' first keys (and the second key of
+//   request pl, which gives P) writes *desc and *seen (pinned host); *same_base
+//   = D when every list starts at one slot and allow_same (a run of Pushes on
+//   one list: the frames path), else UINT64_MAX.
+// run_pass: one lane per row, over rows [0, rows), when the layout (*desc when
+//   desc != NULL — run_classify's — else `given`) is RUN_STRIDED; else it only
+//   raises *flag (when flag != NULL).  mode RUN_CHECK compares every key with
+//   its slot's store key and writes seq into *bad on a mismatch; RUN_APPLY
+//   applies the run (Pushes add, Pulls read, PushPulls both) unless *bad ==
+//   seq, when it writes nothing and raises *flag; RUN_PULL_CHECKED does both
+//   for a run without Pushes (nothing in the store is written, so a mismatch
+//   just raises *flag and the replies are not used).
+enum { RUN_CHECK = 0, RUN_APPLY = 1, RUN_PULL_CHECKED = 2 };
+int run_classify(const uint64_t* K, uint64_t S, const RunFrames& f, int k, int pl, int allow_same, RunDesc* desc,
+                 RunSeen* seen, uint64_t* same_base, hipStream_t st);
+int run_pass(int mode, int dtype, void* store_vals, const uint64_t* K, uint64_t S, const RunFrames& f, int k,
+             uint64_t max_rows, const RunDesc* desc, const RunDesc& given, int* bad, int seq, int* flag,
+             hipStream_t st);
 // Stable LSD radix sort on bits [0, bits) of keys[n], carrying u32 values
 // (iota: the values are the positions 0..n-1 and vals is not read).  Ping-pongs
 // between (keys, vals) and (keys_alt, vals_alt); *result = 0 or 1 names the

@@ -1,0 +1,320 @@
+// psg_runs.hip — a run of queued requests on interleaved key lists, served in
+// one pass over the store.
+//
+// The reference server takes its queued messages one at a time
+// (src/internal/Customer.cpp:52-70) and serves each with its own loop over the
+// request's keys (src/ps/KVApp.h:446-454: `store[key] += val` for a Push,
+// `res.vals[i] = store[key]` for a Pull).  In the reference benchmark's layout
+// (tests/test_kv_app_benchmark.cpp:47-52, tests/test_kv_app.cpp:27) worker r
+// sends the keys kMaxKey / num * i + r, so at nw workers every server's store
+// holds nw lists interleaved key by key, and each request is every nw-th key of
+// the store: on its own it touches every line of the store's keys and values
+// (8 nw + 8 nw bytes of lines per key it sends, against 16).  When the requests
+// of several workers sit in the queue one behind the other, their lists are
+// distinct phases of one period,
+//     keys_j[i] == K[D + p_j + P * i],   p_j distinct, 0 <= p_j < P,
+// hence pairwise disjoint: each store slot belongs to at most one request, no
+// two requests touch one value, and the order of the run changes no result
+// (a Pull reads slots no Push of the run writes).  One pass over the rows
+// D + P * i + [0, P) then serves the whole run and reads and writes each line
+// once:
+//     check (a run with Pushes): request key 8 + store key 8   per key
+//     apply: Push  value 4 + store 8; Pull  store 4 + reply 4  per key
+// i.e. 28 B per pushed key and 24 per pulled key — what one identity request
+// moves — for the whole run.
+//
+// One lane per row: the wave's 64 rows make every request's keys, values and
+// replies one contiguous stream (row i of request j is element i of its
+// arrays), and the row's P slots of the store are P contiguous values and keys,
+// read as 16-B vectors when P is a multiple of the vector width.  The phase ->
+// request map is uniform across the block (LDS).
+//
+// run_classify looks at first keys only (one block, one wave per request); the
+// passes verify every key.  A mismatch anywhere makes the apply write nothing
+// (the check pass's word), so the caller (psg_store_run) serves the run request
+// by request from the store it found.
+#include "psg_internal.h"
+
+namespace psg {
+
+namespace {
+
+__global__ __launch_bounds__(1024) void k_run_classify(const uint64_t* __restrict__ K, uint64_t S, RunFrames f,
+                                                       int k, int pl, int allow_same, RunDesc* __restrict__ desc,
+                                                       RunSeen* __restrict__ seen, uint64_t* __restrict__ same_base) {
+  __shared__ uint64_t pos[kMaxFrames];
+  __shared__ int found[kMaxFrames];
+  __shared__ uint64_t pos2;
+  __shared__ int found2;
+  __shared__ RunDesc d;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < k) {
+    const uint64_t key = f.q[w][0];
+    const uint64_t p = lower_bound_wave(K, S, key);
+    if (lane == 0) {
+      pos[w] = p;
+      found[w] = p < S && K[p] == key;
+    }
+    if (w == pl) {
+      const uint64_t key2 = f.q[w][1];
+      const uint64_t p2 = lower_bound_wave(K, S, key2);
+      if (lane == 0) {
+        pos2 = p2;
+        found2 = p2 < S && K[p2] == key2;
+      }
+    }
+  }
+  if (threadIdx.x < kRunMaxPeriod) d.map[threadIdx.x] = -1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.D = 0;
+    d.rows = 0;
+    d.P = 0;
+    d.cls = RUN_NONE;
+    uint64_t base = UINT64_MAX;
+    bool ok = true;
+    uint64_t D = UINT64_MAX;
+    for (int j = 0; j < k; ++j) {
+      ok = ok && found[j];
+      D = pos[j] < D ? pos[j] : D;
+    }
+    if (ok) {
+      bool same = allow_same != 0;
+      for (int j = 1; j < k; ++j) same = same && pos[j] == pos[0];
+      if (same && f.n[0] <= S - pos[0]) {
+        d.cls = RUN_SAME;
+        d.D = D;
+        base = D;
+      } else if (pl >= 0 && found2 && pos2 > pos[pl] && pos2 - pos[pl] >= 2 && pos2 - pos[pl] <= kRunMaxPeriod) {
+        const uint32_t P = (uint32_t)(pos2 - pos[pl]);
+        bool strided = true;
+        uint64_t rows = 0, span = 0;
+        for (int j = 0; j < k && strided; ++j) {
+          const uint64_t p = pos[j] - D;
+          if (p >= P || d.map[p] >= 0) {
+            strided = false;
+            break;
+          }
+          d.map[p] = (int8_t)j;
+          rows = f.n[j] > rows ? f.n[j] : rows;
+          const uint64_t last = p + (uint64_t)P * (f.n[j] - 1) + 1;
+          span = last > span ? last : span;
+        }
+        if (strided && span <= S - D && rows < 0xffffffffull) {
+          d.cls = RUN_STRIDED;
+          d.D = D;
+          d.P = P;
+          d.rows = rows;
+        }
+      }
+    }
+    *same_base = base;
+  }
+  __syncthreads();
+  // the layout for the passes, and a host-readable copy of it with the first
+  // keys' slots (psg_store_run caches them per list)
+  if (threadIdx.x < sizeof(RunDesc) / 4) {
+    reinterpret_cast<int*>(desc)[threadIdx.x] = reinterpret_cast<const int*>(&d)[threadIdx.x];
+    reinterpret_cast<int*>(&seen->d)[threadIdx.x] = reinterpret_cast<const int*>(&d)[threadIdx.x];
+  }
+  if (threadIdx.x < (unsigned)k) {
+    seen->pos[threadIdx.x] = pos[threadIdx.x];
+    seen->found[threadIdx.x] = found[threadIdx.x];
+  }
+}
+
+template <int DT, int MODE>
+__global__ __launch_bounds__(256) void k_run_pass(typename Elem<DT>::T* __restrict__ store,
+                                                  const uint64_t* __restrict__ K, uint64_t S, RunFrames f,
+                                                  const RunDesc* __restrict__ dp, RunDesc given,
+                                                  int* __restrict__ bad, int seq, int* __restrict__ flag) {
+  using E = Elem<DT>;
+  using T = typename E::T;
+  constexpr int V = E::kVec;
+  // per phase: the request's arrays, its keys, its op (0: no request)
+  __shared__ const uint64_t* sq[kRunMaxPeriod];
+  __shared__ const T* sv[kRunMaxPeriod];
+  __shared__ T* so[kRunMaxPeriod];
+  __shared__ uint32_t sn[kRunMaxPeriod];
+  __shared__ int sop[kRunMaxPeriod];
+  __shared__ int8_t smap[kRunMaxPeriod];
+  __shared__ uint64_t sD, srows;
+  __shared__ uint32_t sP;
+  __shared__ int sgo;
+  const RunDesc* d = dp ? dp : &given;
+  if (threadIdx.x < kRunMaxPeriod) smap[threadIdx.x] = d->map[threadIdx.x];
+  if (threadIdx.x == 0) {
+    sD = d->D;
+    srows = d->rows;
+    sP = d->P;
+    int go = d->cls == RUN_STRIDED;
+    if (MODE == RUN_APPLY && *bad == seq) go = 0;
+    sgo = go;
+    if (!go && flag && blockIdx.x == 0) *flag = 1;
+  }
+  __syncthreads();
+  if (!sgo) return;
+  if (threadIdx.x < kRunMaxPeriod) {
+    const int ph = threadIdx.x;
+    const int mj = ph < (int)sP ? smap[ph] : -1;
+    const uint64_t* q = nullptr;
+    const T* v = nullptr;
+    T* o = nullptr;
+    uint32_t n = 0;
+    int op = 0;
+    // compile-time indices into the kernel argument (no private copy of it)
+#pragma unroll
+    for (int j = 0; j < kMaxFrames; ++j)
+      if (j == mj) {
+        q = f.q[j];
+        v = static_cast<const T*>(f.v[j]);
+        o = static_cast<T*>(f.o[j]);
+        n = (uint32_t)f.n[j];
+        op = f.op[j];
+      }
+    sq[ph] = q;
+    sv[ph] = v;
+    so[ph] = o;
+    sn[ph] = n;
+    sop[ph] = op;
+  }
+  __syncthreads();
+  const uint64_t D = sD, rows = srows;
+  const uint32_t P = sP;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  // 16-B vectors of the store along a row when every row starts on one
+  const bool vec = (D % V) == 0 && (P % V) == 0;
+  int mismatch = 0;
+  for (uint64_t row = (uint64_t)blockIdx.x * kBlock + threadIdx.x; row < rows; row += stride) {
+    const uint64_t base = D + (uint64_t)P * row;
+    const uint32_t r = (uint32_t)row;
+    for (uint32_t c0 = 0; c0 < P; c0 += V) {
+      // phases c0 .. c0 + V - 1 of this row (fewer at the end of a row that
+      // is not a multiple of V: the scalar form)
+      if (vec && base + c0 + V <= S) {
+        int ops[V];
+        bool anyop = false, anypush = false;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const int ph = c0 + e;
+          ops[e] = r < sn[ph] ? sop[ph] : 0;
+          anyop = anyop || ops[e];
+          anypush = anypush || (ops[e] & PSG_PUSH);
+        }
+        if (!anyop) continue;
+        // every load of the chunk first, then the arithmetic, then the writes
+        uint64_t kk[V], qq[V];
+        T x[V];
+        if constexpr (MODE != RUN_APPLY) {
+          const u64x2* kp = reinterpret_cast<const u64x2*>(K + base + c0);
+#pragma unroll
+          for (int h = 0; h < V / 2; ++h) {
+            const u64x2 t = __builtin_nontemporal_load(kp + h);
+            kk[2 * h] = t[0];
+            kk[2 * h + 1] = t[1];
+          }
+#pragma unroll
+          for (int e = 0; e < V; ++e) qq[e] = ops[e] ? __builtin_nontemporal_load(sq[c0 + e] + r) : 0;
+        }
+        if constexpr (MODE != RUN_CHECK) {
+          typedef T tv __attribute__((ext_vector_type(V)));
+          const tv y = __builtin_bit_cast(tv, *reinterpret_cast<const u32x4*>(store + base + c0));
+          T a[V];
+#pragma unroll
+          for (int e = 0; e < V; ++e) a[e] = (ops[e] & PSG_PUSH) ? __builtin_nontemporal_load(sv[c0 + e] + r) : T(0);
+#pragma unroll
+          for (int e = 0; e < V; ++e) x[e] = (ops[e] & PSG_PUSH) ? E::add1(y[e], a[e]) : y[e];
+        }
+        if constexpr (MODE != RUN_APPLY) {
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (ops[e] && qq[e] != kk[e]) mismatch = 1;
+        }
+        if constexpr (MODE != RUN_CHECK) {
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (ops[e] & PSG_PULL) __builtin_nontemporal_store(x[e], so[c0 + e] + r);
+          if (MODE == RUN_APPLY && anypush) {
+            typedef T tv __attribute__((ext_vector_type(V)));
+            tv y;
+#pragma unroll
+            for (int e = 0; e < V; ++e) y[e] = x[e];
+            // the slots of the row no request of the run holds go back
+            // unchanged: only this stream writes the store
+            *reinterpret_cast<u32x4*>(store + base + c0) = __builtin_bit_cast(u32x4, y);
+          }
+        }
+      } else {
+        const uint32_t c1 = c0 + V < P ? c0 + V : P;
+        for (uint32_t ph = c0; ph < c1; ++ph) {
+          const int op = r < sn[ph] ? sop[ph] : 0;
+          if (!op) continue;
+          const uint64_t a = base + ph;
+          if constexpr (MODE != RUN_APPLY) {
+            if (sq[ph][r] != K[a]) mismatch = 1;
+          }
+          if constexpr (MODE != RUN_CHECK) {
+            T x = store[a];
+            if (op & PSG_PUSH) x = E::add1(x, sv[ph][r]);
+            if (op & PSG_PULL) so[ph][r] = x;
+            if (MODE == RUN_APPLY && (op & PSG_PUSH)) store[a] = x;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (MODE != RUN_APPLY) {
+    if (__ballot(mismatch) && (threadIdx.x & 63) == 0) {
+      if (MODE == RUN_CHECK) *bad = seq;
+      else if (flag) *flag = 1;
+    }
+  }
+}
+
+template <int DT>
+int pass_t(int mode, void* store_vals, const uint64_t* K, uint64_t S, const RunFrames& f, uint64_t max_rows,
+           const RunDesc* desc, const RunDesc& given, int* bad, int seq, int* flag, hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  // one lane per row, grid-strided past the stream cap
+  uint64_t b = (max_rows + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t)max_stream_blocks();
+  if (b > cap) b = cap;
+  const unsigned g = b ? (unsigned)b : 1u;
+  switch (mode) {
+    case RUN_CHECK:
+      k_run_pass<DT, RUN_CHECK><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag);
+      break;
+    case RUN_APPLY:
+      k_run_pass<DT, RUN_APPLY><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag);
+      break;
+    default:
+      k_run_pass<DT, RUN_PULL_CHECKED><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag);
+      break;
+  }
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+}  // namespace
+
+int run_classify(const uint64_t* K, uint64_t S, const RunFrames& f, int k, int pl, int allow_same, RunDesc* desc,
+                 RunSeen* seen, uint64_t* same_base, hipStream_t st) {
+  k_run_classify<<<1, 1024, 0, st>>>(K, S, f, k, pl, allow_same, desc, seen, same_base);
+  PSG_HIP(hipGetLastError());
+  return PSG_OK;
+}
+
+int run_pass(int mode, int dtype, void* store_vals, const uint64_t* K, uint64_t S, const RunFrames& f, int k,
+             uint64_t max_rows, const RunDesc* desc, const RunDesc& given, int* bad, int seq, int* flag,
+             hipStream_t st) {
+  (void)k;
+  switch (dtype) {
+    case PSG_F32: return pass_t<PSG_F32>(mode, store_vals, K, S, f, max_rows, desc, given, bad, seq, flag, st);
+    case PSG_F64: return pass_t<PSG_F64>(mode, store_vals, K, S, f, max_rows, desc, given, bad, seq, flag, st);
+    case PSG_F16: return pass_t<PSG_F16>(mode, store_vals, K, S, f, max_rows, desc, given, bad, seq, flag, st);
+    case PSG_BF16: return pass_t<PSG_BF16>(mode, store_vals, K, S, f, max_rows, desc, given, bad, seq, flag, st);
+    default: set_error("unsupported dtype %d", dtype); return PSG_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace psg

@@ -194,6 +194,13 @@ int psg_get_device(int* device) {
   PSG_HIP(hipGetDevice(device));
   return PSG_OK;
 }
+
+int psg_device_pci_bus_id(int device, char* buf, int len) {
+  PSG_REQUIRE(buf && len > 0, PSG_ERR_INVALID, "psg_device_pci_bus_id: null or empty buffer");
+  PSG_HIP(hipDeviceGetPCIBusId(buf, len, device));
+  buf[len - 1] = 0;
+  return PSG_OK;
+}
 int psg_device_sync(void) {
   PSG_HIP(hipDeviceSynchronize());
   return PSG_OK;

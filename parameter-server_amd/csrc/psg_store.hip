@@ -76,6 +76,8 @@ constexpr int kRejRange = 0, kRejUnsorted = 1, kPending = 2, kRejIdent = 3;
 // [kFramesBase, +2): a uint64 — the stretch base of a run of Pushes
 // (psg_store_push_frames, frames_base), read by its check and apply kernels.
 constexpr int kFramesBase = 8;
+// [kRejRun]: a strided run's check pass found a key off its slot (psg_runs.hip)
+constexpr int kRejRun = 4;
 
 // The store-key window of one request tile: [lo, hi) of K brackets every key
 // between the tile's first and last key (lo = lower_bound(K, first), hi =
@@ -3113,6 +3115,193 @@ static int frames_sorted(psg_store* s, const uint64_t* const* keys, const void* 
   return PSG_OK;
 }
 
+// ---- a run of queued requests on interleaved lists (psg_runs.hip) ---------
+// PSG_RUNS_STRIDED=0: psg_store_run never tries the strided pass (A/B).
+static bool strided_on() {
+  static const bool on = [] {
+    const char* e = getenv("PSG_RUNS_STRIDED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+static int run_one_by_one(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
+                          const void* const* vals, void* const* outs, hipStream_t st) {
+  for (int j = 0; j < k; ++j)
+    PSG_TRY(handle_sync(s, ops[j], keys[j], 0, (ops[j] & PSG_PUSH) ? vals[j] : nullptr,
+                        (ops[j] & PSG_PULL) ? outs[j] : nullptr, ns[j], st));
+  return PSG_OK;
+}
+
+// The layout of a run from the slots of its lists' first keys, learnt from
+// earlier strided runs (s->run_pos): every list known at this K generation in
+// one period.  The passes verify every key against it, so a stale or wrong
+// guess only costs a rejected pass.
+static bool run_from_cache(psg_store* s, int k, const uint64_t* const* keys, const uint64_t* ns, RunDesc* d) {
+  uint64_t pos[kMaxFrames];
+  uint32_t P = 0;
+  for (int j = 0; j < k; ++j) {
+    int hit = -1;
+    for (int e = 0; e < 64 && hit < 0; ++e) {
+      const auto& c = s->run_pos[e];
+      if (c.q == keys[j] && c.n == ns[j] && c.gen == s->gen && c.P) hit = e;
+    }
+    if (hit < 0) return false;
+    if (P && s->run_pos[hit].P != P) return false;
+    P = s->run_pos[hit].P;
+    pos[j] = s->run_pos[hit].pos0;
+    s->run_pos[hit].last_use = ++s->run_clock;
+  }
+  uint64_t D = UINT64_MAX, rows = 0;
+  for (int j = 0; j < k; ++j) D = pos[j] < D ? pos[j] : D;
+  memset(d, 0, sizeof(*d));
+  memset(d->map, -1, sizeof(d->map));
+  for (int j = 0; j < k; ++j) {
+    const uint64_t p = pos[j] - D;
+    if (p >= P || d->map[p] >= 0) return false;
+    d->map[p] = (int8_t)j;
+    if (ns[j] > rows) rows = ns[j];
+    if (p + (uint64_t)P * (ns[j] - 1) >= s->size - D) return false;
+  }
+  d->D = D;
+  d->P = P;
+  d->rows = rows;
+  d->cls = RUN_STRIDED;
+  return true;
+}
+
+static void run_remember(psg_store* s, int k, const uint64_t* const* keys, const uint64_t* ns, const RunSeen& seen) {
+  for (int j = 0; j < k; ++j) {
+    int slot = -1;
+    uint64_t oldest = UINT64_MAX;
+    for (int e = 0; e < 64; ++e) {
+      const auto& c = s->run_pos[e];
+      if (c.q == keys[j] && c.n == ns[j]) {
+        slot = e;
+        break;
+      }
+      if (c.last_use < oldest) oldest = c.last_use, slot = e;
+    }
+    auto& c = s->run_pos[slot];
+    c.q = keys[j];
+    c.n = ns[j];
+    c.pos0 = seen.pos[j];
+    c.P = seen.d.P;
+    c.gen = s->gen;
+    c.last_use = ++s->run_clock;
+  }
+}
+
+// One launch sequence tries both one-pass forms, each gated on the device by
+// what run_classify found from the first keys, so the host waits once:
+//   same list (every request a Push on one list starting at one slot):
+//     frames_check + frames_apply, as psg_store_push_frames;
+//   strided (distinct phases of one period): run_pass check + apply, or one
+//     checked pass for a run without Pushes.
+// A run whose lists a pass rejected wrote nothing and is served request by
+// request (a same-list run first through frames_sorted's slot form).  A
+// strided run whose lists the host already knows (run_from_cache) skips the
+// classify kernel: its layout goes to the passes as a kernel argument.
+static int run_sorted(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
+                      const void* const* vals, void* const* outs, hipStream_t st, int* served, bool hinted = true) {
+  bool all_push = true, any_push = false, same_n = true;
+  uint64_t total = 0, max_n = 0;
+  int pl = -1;
+  for (int j = 0; j < k; ++j) {
+    all_push = all_push && ops[j] == PSG_PUSH;
+    any_push = any_push || (ops[j] & PSG_PUSH);
+    same_n = same_n && ns[j] == ns[0];
+    total += ns[j];
+    max_n = ns[j] > max_n ? ns[j] : max_n;
+    if (pl < 0 && ns[j] >= 2) pl = j;
+  }
+  bool try_same = all_push && same_n && ns[0] <= s->size;
+  bool try_strided = strided_on() && pl >= 0 && total <= s->size;
+  // a run with Pulls that was not strided at this K generation: the next few
+  // are served one by one without a try (a run of Pushes always tries: the
+  // same-list pass shares the launch)
+  if (try_strided && !all_push && s->run_fail_gen == s->gen && s->run_fail_count > 0) {
+    --s->run_fail_count;
+    try_strided = false;
+  }
+  // a run of Pushes that could be either form tries the one the last run was
+  // served as first (its other pass would only launch to find itself gated)
+  bool hint_used = false;
+  if (hinted && try_same && try_strided) {
+    if (s->run_last == PSG_RUN_SAME_LIST) try_strided = false, hint_used = true;
+    else if (s->run_last == PSG_RUN_STRIDED) try_same = false, hint_used = true;
+  }
+  if (!try_same && !try_strided) return run_one_by_one(s, k, ops, keys, ns, vals, outs, st);
+  RunFrames f = {};
+  for (int j = 0; j < k; ++j) {
+    f.q[j] = keys[j];
+    f.v[j] = (ops[j] & PSG_PUSH) ? vals[j] : nullptr;
+    f.o[j] = (ops[j] & PSG_PULL) ? outs[j] : nullptr;
+    f.n[j] = ns[j];
+    f.op[j] = ops[j];
+  }
+  RunDesc given;
+  memset(&given, 0, sizeof(given));
+  const bool cached = !try_same && try_strided && run_from_cache(s, k, keys, ns, &given);
+  RunDesc* desc = cached ? nullptr : static_cast<RunDesc*>(s->run_desc);
+  uint64_t* base = reinterpret_cast<uint64_t*>(s->reject_dev + kFramesBase);
+  int* rej = s->reject_dev + kRejIdent;
+  int* bad = s->reject_dev + kRejRun;
+  const int seq = next_seq(s);
+  reset_flags(s);
+  if (!cached)
+    PSG_TRY(run_classify(s->keys, s->size, f, k, try_strided ? pl : -1, try_same ? 1 : 0, desc, s->run_seen, base, st));
+  if (try_same) {
+    PSG_TRY(frames_check(s->keys, base, keys, 0, k, ns[0], rej, seq, st));
+    PSG_TRY(frames_apply(s->dtype, s->vals, s->size, vals, k, ns[0], base, rej, seq, s->flags + F_MISSING, st));
+  }
+  if (try_strided) {
+    if (any_push) {
+      PSG_TRY(run_pass(RUN_CHECK, s->dtype, s->vals, s->keys, s->size, f, k, max_n, desc, given, bad, seq, nullptr,
+                       st));
+      PSG_TRY(run_pass(RUN_APPLY, s->dtype, s->vals, s->keys, s->size, f, k, max_n, desc, given, bad, seq,
+                       s->flags + F_WINMISS, st));
+    } else {
+      PSG_TRY(run_pass(RUN_PULL_CHECKED, s->dtype, s->vals, s->keys, s->size, f, k, max_n, desc, given, bad, seq,
+                       s->flags + F_WINMISS, st));
+    }
+  }
+  PSG_TRY(read_flags(s, st));
+  if (try_same && !s->flags_host[F_MISSING]) {
+    *served = PSG_RUN_SAME_LIST;
+    count_run(s, k);
+    return PSG_OK;
+  }
+  if (try_strided && !s->flags_host[F_WINMISS]) {
+    *served = PSG_RUN_STRIDED;
+    s->counters[PSG_CTR_STRIDED_RUNS]++;
+    s->counters[PSG_CTR_STRIDED_FRAMES] += (uint64_t)k;
+    if (!cached) run_remember(s, k, keys, ns, *s->run_seen);
+    return PSG_OK;
+  }
+  if (cached) {
+    // the lists moved (or their contents changed) since they were learnt:
+    // forget them, and classify afresh (nothing was written)
+    for (auto& c : s->run_pos)
+      for (int j = 0; j < k; ++j)
+        if (c.q == keys[j]) c.P = 0;
+    return run_sorted(s, k, ops, keys, ns, vals, outs, st, served, hinted);
+  }
+  if (try_strided && !all_push) {
+    s->run_fail_gen = s->gen;
+    s->run_fail_count = 8;
+  }
+  // the hinted form did not hold: both, as an unhinted run (nothing was written)
+  if (hint_used) return run_sorted(s, k, ops, keys, ns, vals, outs, st, served, false);
+  if (try_same) {
+    int fused = 0;
+    PSG_TRY(frames_sorted(s, keys, vals, k, ns[0], st, &fused));
+    if (fused) *served = PSG_RUN_SAME_LIST;
+    return PSG_OK;
+  }
+  return run_one_by_one(s, k, ops, keys, ns, vals, outs, st);
+}
+
 static int frames_args(psg_store* s, const void* const* vals_host, int k) {
   PSG_REQUIRE(s && vals_host, PSG_ERR_INVALID, "push frames: null argument");
   PSG_REQUIRE(k >= 1 && k <= kMaxFrames, PSG_ERR_INVALID, "push frames: 1..%d frames, got %d", kMaxFrames, k);
@@ -3171,6 +3360,13 @@ int psg_store_create(int kind, int dtype, uint64_t key_begin, uint64_t key_end, 
   if ((e = hipMalloc((void**)&s->reject_dev, 64)) != hipSuccess ||
       (e = hipMemset(s->reject_dev, 0, 64)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(reject words)", __FILE__, __LINE__));
+  if ((e = hipMalloc(&s->run_desc, sizeof(RunDesc))) != hipSuccess ||
+      (e = hipMemset(s->run_desc, 0, sizeof(RunDesc))) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(run layout)", __FILE__, __LINE__));
+  if ((e = hipHostMalloc((void**)&s->run_seen, sizeof(RunSeen), hipHostMallocMapped | hipHostMallocCoherent)) !=
+      hipSuccess)
+    return fail(hip_fail(e, "hipHostMalloc(run layout seen)", __FILE__, __LINE__));
+  memset(s->run_seen, 0, sizeof(RunSeen));
   constexpr size_t kCtrBytes = (size_t)kRing * (kArriveShards + 1) * kArriveStride * sizeof(uint64_t);
   if ((e = hipMalloc((void**)&s->done_ctr, kCtrBytes)) != hipSuccess ||
       (e = hipMemset(s->done_ctr, 0, kCtrBytes)) != hipSuccess)
@@ -3217,6 +3413,8 @@ int psg_store_destroy(psg_store* s) {
   if (s->flags_host) (void)hipHostFree(s->flags_host);
   if (s->ring_host) (void)hipHostFree(s->ring_host);
   if (s->reject_dev) (void)hipFree(s->reject_dev);
+  if (s->run_desc) (void)hipFree(s->run_desc);
+  if (s->run_seen) (void)hipHostFree(s->run_seen);
   if (s->done_ctr) (void)hipFree(s->done_ctr);
   if (s->done_ev) (void)hipEventDestroy(s->done_ev);
   for (hipEvent_t ev : s->land_ev)
@@ -3436,6 +3634,37 @@ int psg_store_push_frames(psg_store* s, const uint64_t* const* keys_host, uint64
     PSG_TRY(frames_sorted(s, keys_host, vals_host, k, n, st, &fused));
   }
   if (fused_host) *fused_host = fused;
+  return PSG_OK;
+}
+
+int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
+                  const void* const* vals, void* const* outs, psg_stream stream, int* served) {
+  if (served) *served = PSG_RUN_ONE_BY_ONE;
+  PSG_REQUIRE(s && ops && keys && ns, PSG_ERR_INVALID, "psg_store_run: null argument");
+  PSG_REQUIRE(k >= 1 && k <= kMaxFrames, PSG_ERR_INVALID, "psg_store_run: 1..%d requests, got %d", kMaxFrames, k);
+  bool any_push = false, any_pull = false;
+  for (int j = 0; j < k; ++j) {
+    PSG_REQUIRE(ops[j] >= 1 && ops[j] <= 3, PSG_ERR_INVALID, "psg_store_run: bad flags %d of request %d", ops[j], j);
+    PSG_REQUIRE(ns[j] == 0 || keys[j], PSG_ERR_INVALID, "psg_store_run: null keys of request %d", j);
+    any_push = any_push || (ops[j] & PSG_PUSH);
+    any_pull = any_pull || (ops[j] & PSG_PULL);
+    PSG_REQUIRE(!(ops[j] & PSG_PUSH) || ns[j] == 0 || (vals && vals[j]), PSG_ERR_INVALID,
+                "psg_store_run: push without vals (request %d)", j);
+    PSG_REQUIRE(!(ops[j] & PSG_PULL) || ns[j] == 0 || (outs && outs[j]), PSG_ERR_INVALID,
+                "psg_store_run: pull without out buffer (request %d)", j);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  PSG_TRY(drain(s));
+  int sv = PSG_RUN_ONE_BY_ONE;
+  bool empty = false;
+  for (int j = 0; j < k; ++j) empty = empty || ns[j] == 0;
+  if (k == 1 || empty || s->kind != PSG_STORE_SORTED || !sorted_fused() || s->size == 0) {
+    PSG_TRY(run_one_by_one(s, k, ops, keys, ns, vals, outs, st));
+  } else {
+    PSG_TRY(run_sorted(s, k, ops, keys, ns, vals, outs, st, &sv));
+  }
+  s->run_last = sv;
+  if (served) *served = sv;
   return PSG_OK;
 }
 

@@ -68,6 +68,7 @@ class ThreadsafePQueue {
     size_.store(queue_.size(), std::memory_order_release);
     return true;
   }
+  size_t Size() const { return size_.load(std::memory_order_acquire); }
   Message WaitAndPop() {
     SpinFor([this] { return size_.load(std::memory_order_acquire) > 0; });
     std::unique_lock<std::mutex> lk(mu_);
@@ -116,6 +117,8 @@ class Customer {
   bool TakeQueued(Pred take, Message* out) {
     return receive_queue_.PopIf(take, out);
   }
+  /* messages waiting in the receive queue (a hint: it may change at once) */
+  size_t Queued() const { return receive_queue_.Size(); }
 
   int app_id() const { return app_id_; }
   int customer_id() const { return customer_id_; }

@@ -148,6 +148,25 @@ inline bool PushRunsOn() {
   }();
   return on;
 }
+/* PS_MIXED_RUNS=0: a run holds Pushes of one shape only, never the Pulls and
+ * PushPulls of distinct senders queued with them (A/B; KVServer::OnReceive). */
+inline bool MixedRunsOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_MIXED_RUNS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+/* PS_RUN_GATHER_US: how long a server waits for the requests of the senders
+ * it has heard from lately to join a run (KVServer::OnReceive); 0 (default):
+ * a run holds what is queued when it starts. */
+inline int RunGatherMicros() {
+  static const int us = [] {
+    const char* e = std::getenv("PS_RUN_GATHER_US");
+    return e ? std::atoi(e) : 0;
+  }();
+  return us;
+}
 /* PS_TRACE_REQUESTS=<file>: every request a KVServer hands to its handle is
  * appended to <file> as one line "server sender timestamp push pull keys
  * run_size run_pos" (run_size 1 for a request handled on its own) — the
@@ -348,15 +367,22 @@ class KVWorker : public SimpleApp {
   Slicer slicer_;
 };
 
+/* one request of a run of queued requests (KVServer::OnReceive) */
+template <typename Value>
+struct KVRunItem {
+  KVMeta meta;
+  KVPairs<Value> data;
+  SVector<Value> out;  // the output slice a Pull offered for its reply (direct reply), else empty
+};
+
 template <typename Value>
 class KVServer : public SimpleApp {
  public:
   using ReqHandle = std::function<void(const KVMeta& req_meta, const KVPairs<Value>& req_data, KVServer* server)>;
-  /* A run of Pushes queued one behind the other (see OnReceive), in arrival
+  /* A run of requests queued one behind the other (see OnReceive), in arrival
    * order; the handle answers every one of them. */
-  using RunHandle = std::function<void(const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& data,
-                                       KVServer* server)>;
-  static constexpr int kMaxRun = 16;  // requests a run holds at most (psg_store_push_frames)
+  using RunHandle = std::function<void(std::vector<KVRunItem<Value>>& run, KVServer* server)>;
+  static constexpr int kMaxRun = 16;  // requests a run holds at most (psg_store_run)
 
   explicit KVServer(int app_id) : SimpleApp() {
     app_id_ = app_id;
@@ -375,8 +401,7 @@ class KVServer : public SimpleApp {
   /* the default handle keeps its store in HBM and takes frames where they are,
    * and serves a run of queued Pushes on one key list in one pass */
   void SetRequestHandle(const KVServerDefaultHandle<Value>& h) {
-    Install(h, true, [hd = h](const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& data,
-                         KVServer* server) mutable { hd.PushRun(metas, data, server); });
+    Install(h, true, [hd = h](std::vector<KVRunItem<Value>>& run, KVServer* server) mutable { hd.Run(run, server); });
   }
   /* a handle that consumes HBM frames itself */
   void SetDeviceRequestHandle(const ReqHandle& request_handle) {
@@ -386,9 +411,25 @@ class KVServer : public SimpleApp {
 
   /* reply to a request (KVApp.h:491-513); frames may be host or HBM */
   void Response(const KVMeta& req, const KVPairs<Value>& res = KVPairs<Value>());
+  /* For a run handle: reply to one request of a run; `direct` says the handle
+   * wrote the Pull's values into the output slice the request offered
+   * (KVRunItem::out), so the reply carries its keys and no values. */
+  void RunResponse(const KVMeta& req, const KVPairs<Value>& res, bool direct) { Reply(req, res, direct); }
+  /* For a run handle: serve one request of a run with the installed handle, as
+   * if it had been taken on its own (its output offer included). */
+  void ServeOne(const KVRunItem<Value>& item) {
+    direct_out_ = item.out;
+    direct_ts_ = item.meta.timestamp;
+    direct_sender_ = item.meta.sender;
+    direct_taken_ = false;
+    request_handle_(item.meta, item.data, this);
+    direct_out_ = SVector<Value>();
+    direct_taken_ = false;
+  }
 
  private:
   void OnReceive(const Message& msg) override;
+  void Reply(const KVMeta& req, const KVPairs<Value>& res, bool direct);
   void Install(const ReqHandle& h, bool device_frames, const RunHandle& run = nullptr) {
     {
       std::lock_guard<std::mutex> lk(handle_mu_);
@@ -397,6 +438,15 @@ class KVServer : public SimpleApp {
       device_frames_ = device_frames;
     }
     handle_cv_.notify_all();
+  }
+  /* a request a run may hold: a Push, Pull or PushPull with keys and no lens
+   * ([keys, vals], [keys, out] for a Pull offering its output, [keys, vals, out]
+   * for such a PushPull) */
+  static bool PlainRequest(const Message& m) {
+    if (!m.meta.request || m.meta.simple_app || m.meta.control.cmd != Control::EMPTY) return false;
+    if (!(m.meta.push || m.meta.pull)) return false;
+    const size_t want = (m.meta.direct_reply && m.meta.push && m.meta.pull) ? 3 : 2;
+    return m.data.size() == want && m.data[0].size() > 0 && (!m.meta.push || m.data[1].size() > 0);
   }
   static KVMeta MetaOf(const Message& msg) {
     KVMeta meta;
@@ -409,6 +459,23 @@ class KVServer : public SimpleApp {
     return meta;
   }
   RunHandle run_handle_;
+  // the senders of the last requests this server took (the gather window's
+  // target: how many requests one step brings), a ring of 64
+  int recent_[64] = {};
+  unsigned recent_n_ = 0;
+  void NoteSender(int sender) { recent_[recent_n_++ & 63] = sender; }
+  size_t RecentSenders(int sender) {
+    NoteSender(sender);
+    const unsigned n = recent_n_ < 64 ? recent_n_ : 64;
+    int seen[64];
+    size_t c = 0;
+    for (unsigned i = 0; i < n; ++i) {
+      bool dup = false;
+      for (size_t j = 0; j < c && !dup; ++j) dup = seen[j] == recent_[i];
+      if (!dup) seen[c++] = recent_[i];
+    }
+    return c < (size_t)kMaxRun ? c : (size_t)kMaxRun;
+  }
   // The customer thread may receive a request before the program installs its
   // handle (it is created with the KVServer); it waits for the handle instead
   // of failing the reference's CHECK (KVApp.h:487) on that race.
@@ -536,14 +603,92 @@ struct KVServerDefaultHandle {
     server->Response(req_meta, res);
   }
 
-  /* A run of Pushes queued one behind the other (KVServer::OnReceive), with the
-   * result of handling them one at a time in that order (KVApp.h:446-454 per
-   * request).  Full key lists go to psg_store_push_frames, which reads and
-   * writes the store once for the whole run when the lists are one list, and
-   * serves them request by request otherwise.  With the key cache, a run of
-   * requests naming one cached list by its hash is one pass over the cached
-   * slots or stretch (psg_store_push_slots_frames).  Every request is answered
-   * after the run is applied. */
+  /* A run of requests queued one behind the other (KVServer::OnReceive), with
+   * the result of handling them one at a time in that order (KVApp.h:446-454
+   * per request).  Full key lists go to psg_store_run, which reads and writes
+   * the store once for the whole run when the lists are one list (Pushes) or
+   * interleave (distinct phases of one period of the store: the reference
+   * benchmark's layout), and serves them request by request otherwise.  With
+   * the key cache, a run of Pushes naming one cached list by its hash is one
+   * pass over the cached slots or stretch (psg_store_push_slots_frames).
+   * Every request is answered after the run is served. */
+  void Run(std::vector<KVRunItem<Value>>& run, KVServer<Value>* server) {
+    bool all_push = true, hashed = false;
+    for (const auto& it : run) {
+      all_push = all_push && it.meta.push && !it.meta.pull;
+      hashed = hashed || it.data.keys.size() == 1;
+    }
+    if (all_push) {
+      std::vector<KVMeta> metas;
+      std::vector<KVPairs<Value>> datas;
+      for (const auto& it : run) {
+        metas.push_back(it.meta);
+        datas.push_back(it.data);
+      }
+      PushRun(metas, datas, server);
+      return;
+    }
+    if (state->key_cache && hashed) {
+      // a one-key request names a cached list (LRServer.h:129-135): on its own
+      for (const auto& it : run) server->ServeOne(it);
+      return;
+    }
+    const int dev = PostOffice::Get()->device();
+    CHECK_GE(dev, 0) << "KVServerDefaultHandle: the value store lives in HBM and this node has no GPU";
+    constexpr int dt = device::DType<Value>();
+    CHECK_GE(dt, 0) << "KVServerDefaultHandle: value type not supported by the HBM store";
+    if (!state->store)
+      device::Check(psg_store_create(PSG_STORE_SORTED, dt, 0, kMaxKey, 0, &state->store), "psg_store_create");
+    psg_stream s = device::ThreadStream();
+    const size_t k = run.size();
+    std::vector<int> ops(k);
+    std::vector<uint64_t> ns(k);
+    std::vector<SVector<Key>> dkeys(k);
+    std::vector<SVector<Value>> dvals(k), douts(k);
+    std::vector<const uint64_t*> kp(k);
+    std::vector<const void*> vp(k, nullptr);
+    std::vector<void*> op(k, nullptr);
+    std::vector<char> direct(k, 0);
+    for (size_t j = 0; j < k; ++j) {
+      const auto& it = run[j];
+      const size_t n = it.data.keys.size();
+      ops[j] = (it.meta.push ? PSG_PUSH : 0) | (it.meta.pull ? PSG_PULL : 0);
+      ns[j] = n;
+      if (it.meta.push) CHECK_EQ(n, it.data.vals.size());  // one value per key (KVApp.h:441)
+      dkeys[j] = detail::ToDeviceAsync(it.data.keys, dev);
+      kp[j] = dkeys[j].data();
+      if (it.meta.push) {
+        dvals[j] = detail::ToDeviceAsync(it.data.vals, dev);
+        vp[j] = dvals[j].data();
+      }
+      if (it.meta.pull) {
+        direct[j] = it.out.size() == n && it.out.on_device();
+        douts[j] = direct[j] ? it.out : SVector<Value>::OnDevice(n, dev);
+        op[j] = douts[j].data();
+      }
+    }
+    {
+      stage::Scope t("server.handle.store.run");
+      int served = 0;
+      device::Check(psg_store_run(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), op.data(), s,
+                                  &served),
+                    "psg_store_run");
+    }
+    if (state->key_cache)
+      for (size_t j = 0; j < k; ++j)
+        Remember(dkeys[j], run[j].data.keys.on_device(),
+                 run[j].data.keys.on_device() ? 0 : detail::KeyListHash(run[j].data.keys.data(), ns[j]), s);
+    for (size_t j = 0; j < k; ++j) {
+      KVPairs<Value> res;
+      if (run[j].meta.pull) {
+        res.keys = run[j].data.keys;
+        if (!direct[j]) res.vals = run[j].data.keys.on_device() ? douts[j] : detail::ToHost(douts[j]);
+      }
+      server->RunResponse(run[j].meta, res, direct[j] != 0);
+    }
+  }
+
+  /* A run of Pushes of one shape (Run). */
   void PushRun(const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& datas, KVServer<Value>* server) {
     const int dev = PostOffice::Get()->device();
     CHECK_GE(dev, 0) << "KVServerDefaultHandle: the value store lives in HBM and this node has no GPU";
@@ -597,9 +742,12 @@ struct KVServerDefaultHandle {
         kp[j] = dkeys[j].data();
         vp[j] = dvals[j].data();
       }
-      int fused = 0;
-      device::Check(psg_store_push_frames(state->store, kp.data(), 0, vp.data(), (int)k, n, s, &fused),
-                    "psg_store_push_frames");
+      std::vector<int> ops(k, PSG_PUSH);
+      std::vector<uint64_t> ns(k, n);
+      int served = 0;
+      device::Check(psg_store_run(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), nullptr, s,
+                                  &served),
+                    "psg_store_run");
       if (state->key_cache)
         for (size_t j = 0; j < k; ++j)
           Remember(dkeys[j], datas[j].keys.on_device(),
@@ -727,36 +875,69 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       data.lens = detail::ToHost(data.lens);
     }
   }
-  // A run of Pushes.  The reference's receive thread handles the queued
-  // messages one at a time, in queue order (Customer.cpp:52-70); a plain Push
-  // taken here may bring along the Pushes queued right behind it — the very
-  // messages the thread would handle next, so nothing is reordered — when they
-  // have the same shape (push only, as many keys and values, no lens, no reply
-  // offer).  The run's handle (KVServerDefaultHandle::PushRun) serves them as
-  // that sequence: one pass when their key lists are one list (nw workers of
-  // a BSP round), request by request otherwise.
-  if (run && device_frames && detail::PushRunsOn() && meta.push && !meta.pull && !msg.meta.direct_reply && n == 2 &&
-      data.keys.size()) {
+  // A run of queued requests.  The reference's receive thread handles the
+  // queued messages one at a time, in queue order (Customer.cpp:52-70); a
+  // plain request taken here (no lens) may bring along the requests queued
+  // right behind it — the very messages the thread would handle next, so
+  // nothing is reordered — and the run's handle (KVServerDefaultHandle::Run)
+  // serves them as that sequence:
+  //   Pushes of one shape (one pass when their lists are one list: nw workers
+  //     of a BSP round, or a worker's Pushes in flight), and
+  //   requests of distinct senders, Pushes and Pulls (one pass when their
+  //     lists interleave: the reference benchmark's `kMaxKey / num * i + rank`
+  //     at nw workers, tests/test_kv_app_benchmark.cpp:47-52);
+  // request by request otherwise.
+  if (run && device_frames && detail::PushRunsOn() && PlainRequest(msg)) {
     const size_t kbytes = msg.data[0].size(), vbytes = msg.data[1].size();
-    auto mate = [&](const Message& m) {
-      return m.meta.request && !m.meta.simple_app && m.meta.control.cmd == Control::EMPTY && m.meta.push &&
-             !m.meta.pull && !m.meta.direct_reply && m.meta.app_id == msg.meta.app_id && m.data.size() == 2 &&
-             m.data[0].size() == kbytes && m.data[1].size() == vbytes;
+    auto push_shape = [&](const Message& m) {
+      return m.meta.push && !m.meta.pull && !m.meta.direct_reply && m.data.size() == 2 && m.data[0].size() == kbytes &&
+             m.data[1].size() == vbytes;
     };
-    std::vector<KVMeta> metas{meta};
-    std::vector<KVPairs<Value>> datas{data};
+    bool all_push = push_shape(msg), distinct = true;
+    std::vector<KVRunItem<Value>> items(1);
+    items[0].meta = meta;
+    items[0].data = data;
+    items[0].out = direct_out_;
+    auto mate = [&](const Message& m) {
+      if (m.meta.app_id != msg.meta.app_id || !PlainRequest(m)) return false;
+      if (all_push && push_shape(m)) return true;
+      if (!distinct || !detail::MixedRunsOn()) return false;
+      for (const auto& it : items)
+        if (it.meta.sender == m.meta.sender) return false;
+      return true;
+    };
+    // The gather window (PS_RUN_GATHER_US, default 0: off): when fewer
+    // requests are queued than the senders this server has heard from lately,
+    // wait up to that long for theirs to arrive — the requests of one step
+    // reach a server microseconds apart, and a request taken alone costs a
+    // whole pass over the store's lines.  The wait ends as soon as the head of
+    // the queue is a message that may not join.
+    const int gather_us = detail::RunGatherMicros();
+    const size_t want = gather_us > 0 ? RecentSenders(meta.sender) : 0;
+    const auto t_gather = std::chrono::steady_clock::now();
     Message next;
-    while ((int)metas.size() < kMaxRun && customer_->TakeQueued(mate, &next)) {
-      metas.push_back(MetaOf(next));
-      KVPairs<Value> d;
-      d.keys = next.data[0];
-      d.vals = next.data[1];
-      datas.push_back(std::move(d));
+    while ((int)items.size() < kMaxRun) {
+      if (!customer_->TakeQueued(mate, &next)) {
+        if (items.size() >= want || customer_->Queued() > 0) break;
+        if (std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(gather_us)) break;
+        __builtin_ia32_pause();
+        continue;
+      }
+      NoteSender(next.meta.sender);
+      KVRunItem<Value> it;
+      it.meta = MetaOf(next);
+      for (const auto& o : items) distinct = distinct && o.meta.sender != it.meta.sender;
+      all_push = all_push && push_shape(next);
+      it.data.keys = next.data[0];
+      if (next.meta.push) it.data.vals = next.data[1];
+      if (next.meta.direct_reply) it.out = next.data[next.data.size() - 1];
+      items.push_back(std::move(it));
     }
-    if (metas.size() > 1) {
-      for (size_t j = 0; j < metas.size(); ++j)
-        detail::TraceRequest(PostOffice::Get()->my_id(), metas[j], datas[j].keys.size(), metas.size(), j);
-      run(metas, datas, this);
+    if (items.size() > 1) {
+      direct_out_ = SVector<Value>();
+      for (size_t j = 0; j < items.size(); ++j)
+        detail::TraceRequest(PostOffice::Get()->my_id(), items[j].meta, items[j].data.keys.size(), items.size(), j);
+      run(items, this);
       return;
     }
   }
@@ -772,6 +953,13 @@ void KVServer<Value>::OnReceive(const Message& msg) {
 
 template <typename Value>
 void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
+  // the handle wrote this Pull's values into the worker's output in place
+  Reply(req, res,
+        direct_taken_.load() && req.timestamp == direct_ts_.load() && req.sender == direct_sender_.load());
+}
+
+template <typename Value>
+void KVServer<Value>::Reply(const KVMeta& req, const KVPairs<Value>& res, bool direct) {
   stage::Scope t("server.response", res.keys.size() * sizeof(Key) + res.vals.size() * sizeof(Value));
   Message msg;
   msg.meta.app_id = customer_->app_id();
@@ -784,8 +972,7 @@ void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
   msg.meta.receiver = req.sender;
   // tells the worker that HBM frames reach this handle without a copy back
   msg.meta.hbm_handle = device_frames_.load();
-  // the handle wrote this Pull's values into the worker's output in place
-  msg.meta.direct_reply = direct_taken_.load() && req.timestamp == direct_ts_.load() && req.sender == direct_sender_.load();
+  msg.meta.direct_reply = direct;
   if (msg.meta.direct_reply) CHECK(res.vals.empty()) << "a direct reply carries no values";
   if (res.keys.size()) {
     msg.AddData(res.keys);

@@ -26,6 +26,7 @@ LIB_PATH = os.environ.get(
 F32, F64, F16, BF16 = 0, 1, 2, 3
 DENSE, SORTED = 0, 1
 PUSH, PULL = 1, 2
+RUN_ONE_BY_ONE, RUN_SAME_LIST, RUN_STRIDED = 0, 1, 2
 H2D, D2H, D2D = 0, 1, 2
 
 _NP = {F32: np.float32, F64: np.float64, F16: np.float16, BF16: np.uint16}
@@ -33,7 +34,7 @@ _ESIZE = {F32: 4, F64: 8, F16: 2, BF16: 2}
 
 # every symbol include/psg.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "psg_abi_version", "psg_last_error", "psg_device_count", "psg_set_device",
+    "psg_abi_version", "psg_last_error", "psg_device_count", "psg_set_device", "psg_device_pci_bus_id",
     "psg_get_device", "psg_device_sync", "psg_enable_peer_access", "psg_malloc", "psg_free", "psg_host_alloc",
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
     "psg_memset", "psg_copy", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
@@ -43,7 +44,7 @@ EXPORTS = [
     "psg_store_create", "psg_store_destroy", "psg_store_get_info", "psg_store_clear", "psg_store_counters",
     "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots",
     "psg_store_slots_stretch", "psg_store_handle_stretch", "psg_store_sync", "psg_store_dump",
-    "psg_key_list_hash", "psg_store_push_frames", "psg_store_push_slots_frames",
+    "psg_key_list_hash", "psg_store_push_frames", "psg_store_push_slots_frames", "psg_store_run",
     "psg_server_ranges", "psg_slice", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
@@ -89,6 +90,7 @@ def lib() -> C.CDLL:
         sig = {
             "psg_abi_version": ([], i32), "psg_last_error": ([], C.c_char_p),
             "psg_device_count": ([C.POINTER(i32)], i32), "psg_set_device": ([i32], i32),
+            "psg_device_pci_bus_id": ([i32, C.c_char_p, i32], i32),
             "psg_get_device": ([C.POINTER(i32)], i32), "psg_device_sync": ([], i32),
             "psg_enable_peer_access": ([i32, i32], i32),
             "psg_malloc": ([C.POINTER(vp), C.c_size_t], i32), "psg_free": ([vp], i32),
@@ -128,6 +130,8 @@ def lib() -> C.CDLL:
             "psg_store_push_frames": ([vp, C.POINTER(vp), u64, C.POINTER(vp), i32, u64, vp,
                                        C.POINTER(i32)], i32),
             "psg_store_push_slots_frames": ([vp, vp, u64, C.POINTER(vp), i32, u64, vp], i32),
+            "psg_store_run": ([vp, i32, C.POINTER(i32), C.POINTER(vp), C.POINTER(u64), C.POINTER(vp),
+                               C.POINTER(vp), vp, C.POINTER(i32)], i32),
             "psg_server_ranges": ([i32, vp, vp], i32),
             "psg_slice": ([vp, u64, vp, u64, i32, vp, vp, vp, vp, vp], i32),
             "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
@@ -202,6 +206,13 @@ def device_count() -> int:
 
 def set_device(dev: int) -> None:
     _call("psg_set_device", dev)
+
+
+def device_pci_bus_id(dev: int) -> str:
+    """The PCI bus id of GPU `dev` (psg_device_pci_bus_id)."""
+    buf = C.create_string_buffer(64)
+    _call("psg_device_pci_bus_id", dev, buf, 64)
+    return buf.value.decode()
 
 
 def device_sync() -> None:
@@ -371,10 +382,11 @@ class Store:
 
     def counters(self) -> dict:
         """How the store served its keyed requests (psg_store_counters)."""
-        c = (C.c_uint64 * 9)()
-        _call("psg_store_counters", self.h, c, 9)
+        c = (C.c_uint64 * 11)()
+        _call("psg_store_counters", self.h, c, 11)
         return {"fused": c[0], "ident": c[1], "notident": c[2], "ordered": c[3], "runs": c[4],
-                "run_frames": c[5], "coded": c[6], "lean": c[7], "lean_partial": c[8]}
+                "run_frames": c[5], "coded": c[6], "lean": c[7], "lean_partial": c[8],
+                "strided_runs": c[9], "strided_frames": c[10]}
 
     def handle(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> None:
         _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,
@@ -401,6 +413,20 @@ class Store:
         fused = C.c_int(0)
         _call("psg_store_push_frames", self.h, kp, first_key, vp_, k, n, _s(stream), C.byref(fused))
         return bool(fused.value)
+
+    def run(self, ops, keys, ns, vals, outs, stream=None) -> int:
+        """A run of queued requests (psg_store_run): ops[j] PUSH / PULL bits,
+        keys[j] device key arrays of ns[j] keys, vals[j] / outs[j] device arrays
+        (None where the request does not push / pull).  Returns PSG_RUN_*."""
+        k = len(ops)
+        ov = (C.c_int * k)(*ops)
+        kp = (C.c_void_p * k)(*[_ptr(x) for x in keys])
+        nv = (C.c_uint64 * k)(*ns)
+        vp_ = (C.c_void_p * k)(*[_ptr(x) for x in vals])
+        op_ = (C.c_void_p * k)(*[_ptr(x) for x in outs])
+        served = C.c_int(0)
+        _call("psg_store_run", self.h, k, ov, kp, nv, vp_, op_, _s(stream), C.byref(served))
+        return served.value
 
     def push_slots_frames(self, slots, vals, n: int, first: int = 0, stream=None) -> None:
         """A run of len(vals) Pushes on a cached slot list, or (slots None) on
@@ -522,6 +548,12 @@ class Comm:
         self.h = C.c_void_p(None)
         buf = C.create_string_buffer(uid, len(uid))
         _call("psg_comm_init", buf, nranks, rank, C.byref(self.h))
+
+    def rank(self) -> tuple:
+        """(this rank, ranks in the communicator) as RCCL reports them (psg_comm_rank)."""
+        r, n = C.c_int(0), C.c_int(0)
+        _call("psg_comm_rank", self.h, C.byref(r), C.byref(n))
+        return r.value, n.value
 
     def sync(self, stream=None, timeout_s: float = 0.0) -> None:
         """Wait for the queued collectives, at most timeout_s; aborts them and raises on a timeout."""

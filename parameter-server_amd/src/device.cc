@@ -184,7 +184,9 @@ std::shared_ptr<void> HostAlloc(size_t bytes) {
 // fresh block costs its first touch — 2 MiB faults, spread over the copy
 // threads of HostCopy / HostZero (120 MB: ~2 ms on the GPU host against ~10 ms
 // on 4 KiB pages, profiles/r5_probe_host_faults.txt) — and a freed one that
-// would take the pool past PS_HOST_POOL_MB (default 4096) is returned.
+// would take the pool past PS_HOST_POOL_MB (default 1024) is returned.  A
+// request takes the smallest pooled block of its size up to twice it, so
+// frames of varying sizes share blocks instead of each pinning its own class.
 namespace {
 struct HugePool {
   std::mutex mu;
@@ -192,7 +194,7 @@ struct HugePool {
   size_t held = 0;
   size_t cap = [] {
     const char* e = std::getenv("PS_HOST_POOL_MB");
-    const long v = e ? std::atol(e) : 4096;
+    const long v = e ? std::atol(e) : 1024;
     return (size_t)(v < 0 ? 0 : v) << 20;
   }();
 };
@@ -205,16 +207,18 @@ HugePool& Huge() {
 std::shared_ptr<void> HugeAlloc(size_t bytes) {
   constexpr size_t kHuge = size_t(2) << 20;
   if (bytes < 2 * kHuge) return nullptr;
-  const size_t rb = (bytes + kHuge - 1) & ~(kHuge - 1);
+  size_t rb = (bytes + kHuge - 1) & ~(kHuge - 1);
   HugePool& hp = Huge();
   void* p = nullptr;
   {
     std::lock_guard<std::mutex> lk(hp.mu);
-    auto it = hp.free.find(rb);
-    if (it != hp.free.end() && !it->second.empty()) {
+    for (auto it = hp.free.lower_bound(rb); it != hp.free.end() && it->first <= 2 * rb; ++it) {
+      if (it->second.empty()) continue;
       p = it->second.back();
       it->second.pop_back();
-      hp.held -= rb;
+      hp.held -= it->first;
+      rb = it->first;  // the block's own class goes back with it
+      break;
     }
   }
   if (!p) {
@@ -417,6 +421,10 @@ psg_comm* CreateComm(int group) {
 }  // namespace device
 
 namespace {
+// HostFill's byte value that asks for the pages to be faulted in instead
+// (PrefaultHost); MADV_POPULATE_WRITE (Linux 5.14) spelt out for older headers
+constexpr int kPopulate = 0x100;
+constexpr int kMadvPopulateWrite = 23;
 // A persistent pool for large host copies (vector -> SVector, staging blocks).
 // Spawning the helper threads per call cost more than the copy it split: a
 // 16 MiB staging chunk copied by 4 fresh threads spent ~25 us on thread
@@ -467,8 +475,18 @@ class CopyPool {
   static void Part(Job& j, int i) {
     const size_t off = j.chunk * (size_t)i;
     if (off < j.bytes) {
-      if (j.src) std::memcpy(j.dst + off, j.src + off, std::min(j.chunk, j.bytes - off));
-      else std::memset(j.dst + off, j.fill, std::min(j.chunk, j.bytes - off));
+      const size_t len = std::min(j.chunk, j.bytes - off);
+      if (j.src) {
+        std::memcpy(j.dst + off, j.src + off, len);
+      } else if (j.fill == kPopulate) {
+        // fault the part's whole pages in without writing through the
+        // caller's objects (the kernel zero-fills fresh pages anyway)
+        const uintptr_t a = ((uintptr_t)(j.dst + off) + 4095) & ~uintptr_t(4095);
+        const uintptr_t b = ((uintptr_t)(j.dst + off + len)) & ~uintptr_t(4095);
+        if (b > a) (void)madvise((void*)a, b - a, kMadvPopulateWrite);
+      } else {
+        std::memset(j.dst + off, j.fill, len);
+      }
     }
     j.left.fetch_sub(1, std::memory_order_acq_rel);
   }
@@ -538,12 +556,16 @@ void HostFill(void* dst, int byte, size_t bytes) {
 void PrefaultHost(void* p, size_t bytes) {
   if (bytes < kSplit) return;
   // the whole 2 MiB pages inside [p, p + bytes) on huge pages, then every page
-  // written once, in parallel (the caller overwrites it all anyway)
+  // faulted in by the kernel (MADV_POPULATE_WRITE), in parallel — no store
+  // through the caller's memory, which may be a vector's unused capacity
   constexpr uintptr_t kHuge = uintptr_t(2) << 20;
   const uintptr_t a = ((uintptr_t)p + kHuge - 1) & ~(kHuge - 1);
   const uintptr_t b = ((uintptr_t)p + bytes) & ~(kHuge - 1);
   if (b > a) (void)madvise((void*)a, b - a, MADV_HUGEPAGE);
-  HostFill(p, 0, bytes);
+  const int nthreads = CopyThreads();
+  const int parts = (int)std::max<size_t>(1, std::min<size_t>((size_t)nthreads, bytes / kPart));
+  const size_t chunk = (bytes / parts + 4095) & ~size_t(4095);
+  Pool()->Run((char*)p, nullptr, bytes, parts, chunk, kPopulate);
 }
 
 }  // namespace ps

@@ -5,6 +5,7 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/statvfs.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -178,8 +179,9 @@ char* MapBlock(const std::string& base_name, size_t rb, size_t nseg, size_t seg,
 // block of its own as before.
 struct Arena {
   std::mutex mu;
-  std::thread builder;
-  bool started = false, joined = false;
+  bool started = false;
+  std::atomic<bool> ready{false};  // the builder has published base / size / free
+  std::atomic<bool> done{false};   // the builder has finished (built or not)
   char* base = nullptr;
   size_t size = 0;
   std::map<size_t, size_t> free;  // offset -> length, coalesced
@@ -189,10 +191,23 @@ Arena& A() {
   return *a;
 }
 
+// PS_SHM_ARENA_MB sets the size; by default 256 MiB, but never more than a
+// 1/16 of what /dev/shm has free when the van starts (N workers and N servers
+// on one host each build one: 2N arenas must leave room for the frames that do
+// not fit them, and for the message rings).
 size_t ArenaBytes() {
   const char* e = std::getenv("PS_SHM_ARENA_MB");
-  const long mb = e ? std::atol(e) : 256;
-  return mb > 0 ? (size_t)mb << 20 : 0;
+  if (e) {
+    const long mb = std::atol(e);
+    return mb > 0 ? (size_t)mb << 20 : 0;
+  }
+  size_t bytes = (size_t)256 << 20;
+  struct statvfs fs;
+  if (statvfs("/dev/shm", &fs) == 0) {
+    const size_t cap = (size_t)fs.f_bavail * fs.f_frsize / 16;
+    if (cap < bytes) bytes = cap & ~(((size_t)1 << 20) - 1);
+  }
+  return bytes >= ((size_t)16 << 20) ? bytes : 0;
 }
 
 void BuildArena(size_t bytes) {
@@ -206,26 +221,33 @@ void BuildArena(size_t bytes) {
   const size_t nseg = (bytes + seg - 1) / seg;
   const size_t rb = nseg * seg;
   char* p = MapBlock(base_name, rb, nseg, seg, true, true);
-  if (!p) return;  // no room in /dev/shm: every frame takes a block of its own
+  if (!p) {  // no room in /dev/shm: every frame takes a block of its own
+    A().done.store(true, std::memory_order_release);
+    return;
+  }
   Register(p, rb);
   {
     std::lock_guard<std::mutex> lk(s.mu);
     s.own[(uintptr_t)p] = Block{base_name + ":" + std::to_string(nseg) + ":" + std::to_string(seg), rb};
   }
   Arena& a = A();
-  a.base = p;  // published to the takers by their join of this thread
-  a.size = rb;
-  a.free[0] = rb;
+  {
+    std::lock_guard<std::mutex> lk(a.mu);
+    a.base = p;
+    a.size = rb;
+    a.free[0] = rb;
+  }
+  a.ready.store(true, std::memory_order_release);
+  a.done.store(true, std::memory_order_release);
 }
 
+// A frame from the arena, or nullptr — also while the arena is still being
+// built: a request never waits for the builder (its frame takes a block of its
+// own, as without an arena).
 void* ArenaTake(size_t rb) {
   Arena& a = A();
+  if (!a.ready.load(std::memory_order_acquire)) return nullptr;
   std::lock_guard<std::mutex> lk(a.mu);
-  if (!a.started) return nullptr;
-  if (!a.joined) {
-    a.builder.join();
-    a.joined = true;
-  }
   for (auto it = a.free.begin(); it != a.free.end(); ++it) {
     if (it->second < rb) continue;
     const size_t off = it->first, len = it->second;
@@ -262,7 +284,7 @@ void StartArena() {
   Arena& a = A();
   std::lock_guard<std::mutex> lk(a.mu);
   if (a.started) return;
-  a.builder = std::thread(BuildArena, bytes);
+  std::thread(BuildArena, bytes).detach();  // the arena lives as long as the process
   a.started = true;
 }
 }  // namespace
@@ -355,11 +377,12 @@ char* Map(const std::string& name, size_t* size) {
 void UnlinkAll() {
   {
     Arena& a = A();  // a builder still creating segments would leave names behind
-    std::lock_guard<std::mutex> lk(a.mu);
-    if (a.started && !a.joined) {
-      a.builder.join();
-      a.joined = true;
+    bool started;
+    {
+      std::lock_guard<std::mutex> lk(a.mu);
+      started = a.started;
     }
+    while (started && !a.done.load(std::memory_order_acquire)) std::this_thread::yield();
   }
   State& s = S();
   std::lock_guard<std::mutex> lk(s.mu);

@@ -16,6 +16,9 @@
 // prints
 //   {"rank", "n", "workers", "servers", "layout", "steps", "warmup",
 //    "ms_per_step", "push_ms", "pull_ms", "mismatches"}
+// and each server, at exit, its store's counters (which paths served the
+// requests: {"server", "fused", "ident", "runs", "run_frames", "strided_runs",
+// "strided_frames"}).
 // usage: kv_bench_dropin [-ns S] [-nw W] [-procs] num_keys steps warmup layout
 #include <chrono>
 #include <cstdio>
@@ -31,8 +34,21 @@ int main(int argc, char* argv[]) {
   Start(0, argc, argv);
   if (IsServer()) {
     auto server = new KVServer<float>(0);
-    server->SetRequestHandle(KVServerDefaultHandle<float>());
-    RegisterExitCallback([server]() { delete server; });
+    KVServerDefaultHandle<float> h;
+    server->SetRequestHandle(h);
+    const int id = PostOffice::Get()->my_id();
+    RegisterExitCallback([server, h, id]() {
+      // how the store served the job's requests (psg_store_counters)
+      uint64_t c[PSG_NCOUNTERS] = {};
+      if (h.store()) device::Check(psg_store_counters(h.store(), c, PSG_NCOUNTERS), "psg_store_counters");
+      std::printf("{\"server\": %d, \"fused\": %llu, \"ident\": %llu, \"runs\": %llu, \"run_frames\": %llu, "
+                  "\"strided_runs\": %llu, \"strided_frames\": %llu}\n",
+                  id, (unsigned long long)c[PSG_CTR_FUSED], (unsigned long long)c[PSG_CTR_IDENT],
+                  (unsigned long long)c[PSG_CTR_RUNS], (unsigned long long)c[PSG_CTR_RUN_FRAMES],
+                  (unsigned long long)c[PSG_CTR_STRIDED_RUNS], (unsigned long long)c[PSG_CTR_STRIDED_FRAMES]);
+      std::fflush(stdout);
+      delete server;
+    });
   }
   if (IsWorker()) {
     const long num = argc > 4 ? std::atol(argv[4]) : 10000000;

@@ -39,6 +39,13 @@ class CpuCollectiveBackend:
         import torch
         self.torch, self.rank, self.world, self.dist = torch, rank, world, dist
 
+    def describe(self):
+        # the fields a GPU rank reports (bench.GpuBackend.describe): here the
+        # CPU process, and the gloo group in place of RCCL
+        import socket
+        return {"rank": self.rank, "device": "cpu", "pci_bus_id": None, "host": socket.gethostname(),
+                "rccl_rank": self.dist.get_rank(), "rccl_nranks": self.dist.get_world_size()}
+
     def setup(self, L, seed):
         import oracle
         self.L, self.blk = L, L // self.world
@@ -131,6 +138,13 @@ def test_bench_distributed_path_gloo(world):
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in r0
+    # the N > 1 line names every rank's device, GPU and communicator view
+    ranks = r0["config"]["ranks"]
+    assert [d["rank"] for d in ranks] == list(range(world))
+    for d in ranks:
+        assert {"device", "pci_bus_id", "host", "rccl_rank", "rccl_nranks"} <= set(d)
+        assert d["rccl_nranks"] == world and d["rccl_rank"] == d["rank"]
+    assert "distinct_gpus" in r0["config"] and "calibration_ms" in r0["config"]
 
 
 def _group_rank(rank, world, port, q):

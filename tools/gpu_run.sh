@@ -16,6 +16,8 @@
 #   pmcks    PMC traffic of the key-cached Push on a stretch of slots (k_dense_vec, 12 B/key)
 #   lr       LR apply roofline (tools/bench_lr.py, 10 M and 64 M features) + its rocprof stats
 #   lrb      the bench line of the LR BSP round (bench.py --workload lr) + its rocprof stats
+#   dropin:N:MODE:LAYOUT  the drop-in API line at ns = nw = N (MODE threads|procs,
+#            LAYOUT 0 the benchmark's interleaved keys, 1 one shared list)
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
 #            (tools/pmc_targets.py, two passes each)
 set -u
@@ -78,6 +80,23 @@ for st in "$@"; do
     shared2|shared8)
           nr=${st#shared}; port=$((29500 + RANDOM % 1000))
           PSG_BENCH_SHARE_GPU=1 step 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $nr --master-addr 127.0.0.1 --master-port $port bench.py --gpus $nr > gpurun_out/bench_shared_n$nr.json 2> gpurun_out/bench_shared_n$nr.err; echo "$st rc=$?"; grep "^{" gpurun_out/bench_shared_n$nr.json | cut -c1-600 ;;
+    dropin:*)
+          # dropin:N:mode:layout — the drop-in API line (bench.py --workload dropin)
+          IFS=: read -r _ dn dm dl <<< "$st"; tag="n${dn}_${dm}_l${dl}"
+          step 300 python3 bench.py --workload dropin --gpus "$dn" --dropin-mode "$dm" --dropin-layout "$dl" --no-cpu-baseline > gpurun_out/bench_dropin_$tag.json 2> gpurun_out/bench_dropin_$tag.err; echo "$st rc=$?"; cut -c1-900 gpurun_out/bench_dropin_$tag.json; tail -3 gpurun_out/bench_dropin_$tag.err ;;
+    dtrace:*)
+          # dtrace:N:mode:layout — kv_bench_dropin with the servers' request trace:
+          # run sizes per server (PS_TRACE_REQUESTS) and the store counters
+          IFS=: read -r _ dn dm dl <<< "$st"; tag="n${dn}_${dm}_l${dl}"; rm -f gpurun_out/dtrace_$tag.txt
+          md=""; [ "$dm" = procs ] && md="-procs"
+          PS_TRACE_REQUESTS=$PWD/gpurun_out/dtrace_$tag.txt step 200 tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dtrace_$tag.log 2>&1; echo "$st rc=$?"; grep "^{" gpurun_out/dtrace_$tag.log | cut -c1-300
+          python3 tools/run_sizes.py gpurun_out/dtrace_$tag.txt ;;
+    dprof:*)
+          # dprof:N:mode:layout — rocprof kernel stats + trace of kv_bench_dropin
+          IFS=: read -r _ dn dm dl <<< "$st"; tag="n${dn}_${dm}_l${dl}"; rm -rf gpurun_out/dprof_$tag
+          md=""; [ "$dm" = procs ] && md="-procs"
+          step 240 rocprofv3 --kernel-trace --stats -d gpurun_out/dprof_$tag -o run --output-format csv -- tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dprof_$tag.log 2>&1; echo "$st rc=$?"; grep '"rank": 0' gpurun_out/dprof_$tag.log | cut -c1-300
+          f=$(find gpurun_out/dprof_$tag -name "*kernel_stats.csv" | head -1); cut -c1-180 "$f" | head -12 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
