@@ -913,7 +913,24 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
         backend.sync()
         batched = {"requests": BATCHED, "push_ms": round(backend.elapsed(a, b) / BATCHED, 5),
                    "step_ms": round(backend.elapsed(b, c) / BATCHED, 5)}
-        extra_pushes += 2 * BATCHED
+        # ... next to the same Pushes with a marker between every two (the
+        # per-request line's timing) and to the markers alone (VERDICT r5 next
+        # #4): marker_ms is what one marker adds to the stream, so
+        # per_request_push_ms - push_ms should equal it if markers explain the gap
+        em = [backend.new_event() for _ in range(BATCHED + 1)]
+        backend.record(em[0])
+        for i in range(BATCHED):
+            backend.push()
+            backend.record(em[i + 1])
+        mk = [backend.new_event() for _ in range(BATCHED + 1)]
+        for e in mk:
+            backend.record(e)
+        backend.sync()
+        batched["per_request_push_ms"] = round(sum(backend.elapsed(em[i], em[i + 1]) for i in range(BATCHED))
+                                               / BATCHED, 5)
+        batched["marker_ms"] = round(backend.elapsed(mk[0], mk[-1]) / BATCHED, 5)
+        batched["gap_ms"] = round(batched["per_request_push_ms"] - batched["push_ms"], 5)
+        extra_pushes += 3 * BATCHED
     total_pushes = args.warmup + args.steps + extra_pushes
     chk = None
     if args.check:
@@ -1024,7 +1041,12 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
             batched["step_gbs"] = round(2 * vb * L / (batched["step_ms"] * 1e-3) / 1e9, 1)
             batched["what"] = (f"{BATCHED} Pushes back to back, then {BATCHED} Push -> Pull steps, each batch "
                                "between one pair of timing-only events: the per-request cost of a steady "
-                               "request stream, dispatch included, without a marker per request")
+                               "request stream, dispatch included, without a marker per request; "
+                               f"per_request_push_ms: {BATCHED} Pushes with a marker after each; marker_ms: "
+                               f"{BATCHED + 1} markers recorded back to back with no kernel, per marker; "
+                               "gap_ms = per_request_push_ms - push_ms")
+            batched["per_request_push_frac"] = round(STRETCH_PUSH_BYTES * L / (batched["per_request_push_ms"]
+                                                                                * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             res["roofline"]["batched"] = batched
     elif world == 1 and getattr(backend, "cached", False):
         res["roofline"] = roofline(CACHED_PUSH_BYTES * L, push_ms, args,
@@ -1189,6 +1211,19 @@ def run_lr(args) -> dict:
             merged = (merged + g).astype(np.float32)
         oracle.lr_apply(ref, merged, 0.01, m, v, lr, 0.9, 0.999, 1e-8, r)
     bad = int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32)))
+    # The copy ceiling of this byte mix: the same kernel's
+    # loads and stores with a copy's arithmetic (psg_lr_mix_copy), timed the
+    # same way in this process, after the parity sample was read (it
+    # scribbles on the weights and moments).
+    cev = [p.Event(timing=TIMING_EVENTS) for _ in range(args.steps + 1)]
+    for _ in range(2):
+        p.lr_mix_copy(w, grads, n, adam, stream=st)
+    cev[0].record(st)
+    for i in range(args.steps):
+        p.lr_mix_copy(w, grads, n, adam, stream=st)
+        cev[i + 1].record(st)
+    st.sync()
+    copy_ms = sum(cev[i].elapsed_ms(cev[i + 1]) for i in range(args.steps)) / args.steps
     adam.close()
     w.close()
     for g in grads:
@@ -1208,6 +1243,12 @@ def run_lr(args) -> dict:
         "roofline": roofline(per * n, kernel_ms, args, "k_lr_apply_sum<ADAM> (merge + Adam, one launch)", 4),
         "event_markers": ("timing-only (hipEventDisableSystemFence)" if TIMING_EVENTS
                           else "default (system-scope fence at each record)"),
+        "copy_ceiling": {"kernel": "k_lr_apply_sum<ADAM, COPY> (psg_lr_mix_copy): the same loads and stores "
+                                   "with a copy's arithmetic",
+                         "ms": round(copy_ms, 5),
+                         "gbs": round(per * n / (copy_ms * 1e-3) / 1e9, 1),
+                         "frac": round(per * n / (copy_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "adam_of_copy": round(copy_ms / kernel_ms, 4)},
     }
     if not args.no_cpu_baseline:
         # the same round restated in oracle/ on one core, on a bounded sample

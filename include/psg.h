@@ -214,7 +214,12 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * (psg_store_run, PSG_RUN_STRIDED), and the requests those runs held */
 #define PSG_CTR_STRIDED_RUNS 9
 #define PSG_CTR_STRIDED_FRAMES 10
-#define PSG_NCOUNTERS 11
+/* lean Pushes validated against their list's verified copy (k_list_check: the
+ * list as a learning request of this K validated it), and those that were not
+ * that list after all and ran again with the full validation */
+#define PSG_CTR_LISTS 11
+#define PSG_CTR_NOTLIST 12
+#define PSG_NCOUNTERS 13
 int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):
@@ -607,6 +612,14 @@ int psg_lr_apply(psg_store* weights, const float* merged, uint64_t n, float lr,
 int psg_lr_apply_sum(psg_store* weights, const float* const* grads_host, int ngrads,
                      int from_zero, uint64_t n, float lr, psg_adam* adam, int iteration,
                      psg_stream stream);
+/* Measurement only (no reference counterpart): psg_lr_apply_sum's Adam pass
+ * (from_zero) with its loads and stores unchanged and a copy's arithmetic in
+ * place of the update (m += s, v -= s, w += s) — the rate this box moves the
+ * Adam apply's byte mix (4 B per frame + weight 8 + f64 moments 32 per
+ * feature), the ceiling bench.py --workload lr compares the apply with.  It
+ * scribbles on the weights and moments. */
+int psg_lr_mix_copy(psg_store* weights, const float* const* grads_host, int ngrads, uint64_t n, psg_adam* adam,
+                    psg_stream stream);
 /* Multi-GPU LR BSP Push (nw = ns = nranks, weights = rank r's f32 DENSE shard
  * of n_total / nranks features, adam = that shard's state):
  *   psg_comm_lr_push  reduce-scatter of every rank's grads[n_total] (RCCL; its

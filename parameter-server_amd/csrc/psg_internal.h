@@ -181,6 +181,7 @@ struct InflightReq {
   int seq;        // its sequence number (reject words, tile words)
   uint32_t tw_ring;  // the ring slot whose tile words its validation wrote (a follow-up keeps it)
   int lean;       // applied by k_tile_apply (its stretch and coded tiles; general ones follow up)
+  int vl;         // 1: validated as its list's verified copy (k_list_check); 2: a learning request
 };
 constexpr int kRing = 64;  // completion words per store (requests in flight + 1)
 struct RunSeen;            // psg_runs.hip (below)
@@ -253,6 +254,13 @@ struct psg_store {
     uint64_t ident_trial;  // ticket of the identity attempt in flight before either is known (0: none)
     int nt;              // the block size (tile size / 4) its windows were filled for
     uint32_t lean_fail;  // K's generation at which a k_tile_apply on this list left general tiles
+    // the verified copy of the list (k_validate_code's learn, k_list_check):
+    // the keys a learning request validated, valid while K keeps copy_gen
+    uint64_t* copy;
+    uint64_t copy_cap;      // keys it holds room for
+    uint32_t copy_gen;      // K's generation it was validated against (0: none)
+    uint32_t vl_fail;       // K's generation at which a Push of this list differed from its copy
+    uint64_t learn_ticket;  // the last learning request launched (its reap validates the copy)
   } wc[4];
   uint64_t wc_clock;
   uint64_t counters[PSG_NCOUNTERS];  // psg_store_counters
@@ -301,9 +309,11 @@ struct Grads {
 // weights[w_off + i] -= update(sum_k grads[k][i]) for i < n, Adam state at
 // adam_off; the merge and the apply of LRServer.h:158-177 in one pass.
 // psg_lr.hip.
+// copy_mix (psg_lr_mix_copy, measurement only): the same pass with a copy's
+// arithmetic in place of the Adam update.
 int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, int ngrads,
                  int from_zero, uint64_t n, float lr, psg_adam* adam, uint64_t adam_off,
-                 int iteration, hipStream_t st);
+                 int iteration, hipStream_t st, bool copy_mix = false);
 // Dense element-wise request on slot range [off, off + n) of a store value
 // array.  op = PSG_PUSH | PSG_PULL bits.  Implemented in psg_dense.hip.
 int dense_request(int dtype, int op, void* store_vals, const void* vals, void* out,

@@ -78,7 +78,10 @@ __device__ __forceinline__ double* mom_v(double* m, double* v, uint64_t i) {
 // exactly MAXG frames (1..4: every slot loaded, no run-time frame test, so the
 // registers of absent frames are not held), else up to kMaxGrads (ng at run
 // time).  LAY: the moment layout (1, 2: m is the one array, v unused).
-template <bool ADAM, bool ZERO, int MAXG, int LAY, bool EXACT>
+// COPY (measurement only, psg_lr_mix_copy): the same loads and stores with a
+// copy's arithmetic (m += g, v -= g, w += g): this kernel's byte mix at the
+// rate the box moves it, the ceiling the Adam apply is compared with.
+template <bool ADAM, bool ZERO, int MAXG, int LAY, bool EXACT, bool COPY = false>
 __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Grads g, int ng, uint64_t n,
                                                       float lr, double* __restrict__ m,
                                                       double* __restrict__ v, double alr, double b1,
@@ -138,6 +141,12 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
           if (EXACT || k < ng) s = s + x[t][k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
+          if constexpr (COPY) {
+            mo[t][e >> 1][e & 1] += (double)s[e];
+            mo[t][2 + (e >> 1)][e & 1] -= (double)s[e];
+            wv[t][e] += s[e];
+            continue;
+          }
           const double gr = (double)(lr * s[e]);
           const double mi = b1 * mo[t][e >> 1][e & 1] + (1.0 - b1) * gr;
           const double vi = b2 * mo[t][2 + (e >> 1)][e & 1] + (1.0 - b2) * gr * gr;
@@ -206,6 +215,12 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
             if (EXACT || k < ng) s = s + x[t][k][h];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
+            if constexpr (COPY) {
+              mm[t][h][e] += (double)s[e];
+              vv[t][h][e] -= (double)s[e];
+              wv[t][h][e] += s[e];
+              continue;
+            }
             const double gr = (double)(lr * s[e]);
             const double mi = b1 * mm[t][h][e] + (1.0 - b1) * gr;
             const double vi = b2 * vv[t][h][e] + (1.0 - b2) * gr * gr;
@@ -226,7 +241,12 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
     float s = ZERO ? 0.0f + g.p[0][i] : g.p[0][i];
     for (int k = 1; k < ng; ++k) s = s + g.p[k][i];
     double grad = (double)(lr * s);
-    if constexpr (ADAM) {
+    if constexpr (ADAM && COPY) {
+      *mom_m<LAY>(m, i) += (double)s;
+      *mom_v<LAY>(m, v, i) -= (double)s;
+      w[i] += s;
+      continue;
+    } else if constexpr (ADAM) {
       double* mi_p = mom_m<LAY>(m, i);
       double* vi_p = mom_v<LAY>(m, v, i);
       const double mi = b1 * *mi_p + (1.0 - b1) * grad;
@@ -241,7 +261,7 @@ __global__ __launch_bounds__(256) void k_lr_apply_sum(float* __restrict__ w, Gra
 
 int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, int ngrads,
                  int from_zero, uint64_t n, float lr, psg_adam* adam, uint64_t adam_off,
-                 int iteration, hipStream_t st) {
+                 int iteration, hipStream_t st, bool copy_mix) {
   PSG_REQUIRE(weights && weights->kind == PSG_STORE_DENSE && weights->dtype == PSG_F32,
               PSG_ERR_INVALID, "LR apply: weights must be an f32 DENSE store");
   PSG_REQUIRE(w_off <= weights->capacity && n <= weights->capacity - w_off, PSG_ERR_RANGE,
@@ -302,8 +322,18 @@ int lr_apply_sum(psg_store* weights, uint64_t w_off, const float* const* grads, 
   auto go = [&](auto adam_c, auto zero_c, auto lay_c) {
     constexpr bool A = decltype(adam_c)::value, Z = decltype(zero_c)::value;
     constexpr int B = decltype(lay_c)::value;
-#define PSG_LR_LAUNCH(G, X) \
-  k_lr_apply_sum<A, Z, G, B, X><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm)
+#define PSG_LR_LAUNCH(G, X)                                                                                    \
+  do {                                                                                                         \
+    if constexpr (A && Z) {                                                                                    \
+      if (copy_mix) {                                                                                          \
+        k_lr_apply_sum<A, Z, G, B, X, true>                                                                    \
+            <<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, ve, ntm);           \
+        break;                                                                                                 \
+      }                                                                                                        \
+    }                                                                                                          \
+    k_lr_apply_sum<A, Z, G, B, X><<<grid, kBlock, 0, st>>>(w, g, ngrads, n, lr, m, v, alr, b1, b2, eps, c1, c2, \
+                                                           ve, ntm);                                           \
+  } while (0)
     switch (ngrads) {
       case 1: PSG_LR_LAUNCH(1, true); break;
       case 2: PSG_LR_LAUNCH(2, true); break;
@@ -399,6 +429,12 @@ int psg_lr_apply_sum(psg_store* weights, const float* const* grads_host, int ngr
                      uint64_t n, float lr, psg_adam* adam, int iteration, psg_stream stream) {
   return lr_apply_sum(weights, 0, grads_host, ngrads, from_zero, n, lr, adam, 0, iteration,
                       (hipStream_t)stream);
+}
+
+int psg_lr_mix_copy(psg_store* weights, const float* const* grads_host, int ngrads, uint64_t n, psg_adam* adam,
+                    psg_stream stream) {
+  PSG_REQUIRE(adam, PSG_ERR_INVALID, "psg_lr_mix_copy: the Adam byte mix needs the moments");
+  return lr_apply_sum(weights, 0, grads_host, ngrads, 1, n, 0.0f, adam, 0, 0, (hipStream_t)stream, true);
 }
 
 }  // extern "C"

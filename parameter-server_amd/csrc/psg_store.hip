@@ -64,7 +64,16 @@ __device__ __forceinline__ void raise_flag(int* flags, int which, bool cond) {
 // The fused keyed request (k_resolve_apply) reports through ONE word of the
 // store's ring in pinned host memory: bits [8, 32) the request's 24-bit tag,
 // bits [0, 8) its flags:
-enum { W_MISSING = 1, W_WINMISS = 2, W_RANGE = 4, W_UNSORTED = 8, W_GATED = 16, W_NOTIDENT = 32, W_PARTIAL = 64 };
+enum {
+  W_MISSING = 1,
+  W_WINMISS = 2,
+  W_RANGE = 4,
+  W_UNSORTED = 8,
+  W_GATED = 16,
+  W_NOTIDENT = 32,
+  W_PARTIAL = 64,
+  W_NOTLIST = 128
+};
 // Device words (reject_dev): the validation pass writes a request's sequence
 // number into [kRejRange] / [kRejUnsorted] when a key is out of the shard's
 // range / out of order.  [kPending] != 0: an earlier request needs the host
@@ -78,6 +87,9 @@ constexpr int kRejRange = 0, kRejUnsorted = 1, kPending = 2, kRejIdent = 3;
 constexpr int kFramesBase = 8;
 // [kRejRun]: a strided run's check pass found a key off its slot (psg_runs.hip)
 constexpr int kRejRun = 4;
+// [kRejList]: a Push sent as its list's verified copy was not that list
+// (k_list_check; the lean apply then writes nothing and reports W_NOTLIST)
+constexpr int kRejList = 5;
 
 // The store-key window of one request tile: [lo, hi) of K brackets every key
 // between the tile's first and last key (lo = lower_bound(K, first), hi =
@@ -179,7 +191,7 @@ __device__ __forceinline__ void request_done(uint64_t after, const Arrival& a, u
   // all of a counter's accesses); the set is next used kRing requests later
   for (int k = 0; k <= kArriveShards; ++k)
     (void)__hip_atomic_exchange(a.ctr + k * kArriveStride, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!(f & (W_GATED | W_RANGE)) && (f & (W_MISSING | W_UNSORTED | W_NOTIDENT | W_PARTIAL)))
+  if (!(f & (W_GATED | W_RANGE)) && (f & (W_MISSING | W_UNSORTED | W_NOTIDENT | W_PARTIAL | W_NOTLIST)))
     __hip_atomic_store(pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(word, tag_bits | f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -558,7 +570,8 @@ __global__ __launch_bounds__(1024, 8) void k_validate_code(const uint64_t* __res
                                                            const Win* __restrict__ win, uint32_t gen, uint64_t kb,
                                                            uint64_t ke, int* __restrict__ reject, int seq, int vec,
                                                            uint32_t* __restrict__ tword,
-                                                           uint32_t* __restrict__ codes) {
+                                                           uint32_t* __restrict__ codes,
+                                                           uint64_t* __restrict__ learn) {
   constexpr int NT = 1024;
   constexpr uint64_t tileN = (uint64_t)NT * kPerLane;
   constexpr uint32_t winN = 2 * NT * kPerLane;
@@ -596,6 +609,18 @@ __global__ __launch_bounds__(1024, 8) void k_validate_code(const uint64_t* __res
     } else {
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) key[k] = i0 + k < t1 ? q[i0 + k] : 0;
+    }
+    // a learning request keeps the list it validates (the verified copy a
+    // later request of this list is compared with, k_list_check)
+    if (learn) {
+      if (i0 + kPerLane <= t1) {
+        reinterpret_cast<u64x2*>(learn + i0)[0] = u64x2{key[0], key[1]};
+        reinterpret_cast<u64x2*>(learn + i0)[1] = u64x2{key[2], key[3]};
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k)
+          if (i0 + k < t1) learn[i0 + k] = key[k];
+      }
     }
     // the store keys to compare with: a stretch tile's K[lo + i], a coded
     // candidate's at its code's places (gathered: the same lines of K)
@@ -732,6 +757,52 @@ __global__ __launch_bounds__(1024, 8) void k_validate_code(const uint64_t* __res
   if (__ballot(unsorted) && lane == 0) reject[kRejUnsorted] = seq;
 }
 
+// The validation of a Push whose key list is its verified copy (the lean
+// apply's first pass instead of k_validate_code): the request keys compared
+// with the copy a learning request of this list kept (k_validate_code's learn)
+// — a plain two-stream compare, 16 B per key, instead of the store keys'
+// lines at the coded places (8 / density) and the lane codes (1).  Keys equal
+// to a list validated against this very K (its generation) are in range,
+// ascending and at the places the cached windows and codes give, so each
+// tile's word is its kind from its window alone: a stretch when the window is
+// exactly the tile, else coded.  Any difference writes seq into
+// rej[kRejList]: the lean apply then writes nothing and the host validates
+// the request in full (W_NOTLIST).  One lane per 4 keys, grid-strided; the
+// tile words by the lanes of each tile's first keys.
+__global__ __launch_bounds__(256) void k_list_check(const uint64_t* __restrict__ q,
+                                                    const uint64_t* __restrict__ copy, uint64_t n,
+                                                    const Win* __restrict__ win, uint32_t gen,
+                                                    int* __restrict__ rej, int seq, int vec,
+                                                    uint32_t* __restrict__ tword) {
+  constexpr uint64_t tileN = 1024 * kPerLane;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  int bad = 0;
+  const uint64_t nq = (n + 3) / 4;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nq; j += stride) {
+    const uint64_t i0 = 4 * j;
+    if (i0 + 4 <= n && vec) {
+      const u64x2 a0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0));
+      const u64x2 a1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0) + 1);
+      const u64x2 b0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(copy + i0));
+      const u64x2 b1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(copy + i0) + 1);
+      if (a0[0] != b0[0] || a0[1] != b0[1] || a1[0] != b1[0] || a1[1] != b1[1]) bad = 1;
+    } else {
+      for (uint64_t i = i0; i < n && i < i0 + 4; ++i)
+        if (q[i] != copy[i]) bad = 1;
+    }
+    if ((i0 % tileN) == 0) {
+      const uint64_t tile = i0 / tileN;
+      const uint64_t t1 = (i0 + tileN < n) ? i0 + tileN : n;
+      const Win e = win[tile];
+      const bool cur = e.gen == gen && e.lo <= e.hi;
+      const uint64_t W = cur ? (uint64_t)(e.hi - e.lo) : 0;
+      if (!cur || W < t1 - i0 || W > 2 * tileN) bad = 1;
+      tword[tile] = tile_tag(seq) | (W == t1 - i0 ? kTileStretch : kTileCoded);
+    }
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) rej[kRejList] = seq;
+}
+
 // The apply of a Push whose validation pass (k_validate_code) sorted its tiles,
 // for the tiles that need no search: a stretch at slots lo + i, a coded tile at
 // the places of its lane codes, its stretch of values staged into LDS, updated
@@ -764,6 +835,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_apply(uint64_t n, const Win* _
   uint32_t uniform = rej[kPending] != 0 ? (uint32_t)W_GATED : 0u;
   if (rej[kRejRange] == seq) uniform |= W_RANGE;
   if (rej[kRejUnsorted] == seq) uniform |= W_UNSORTED;
+  if (rej[kRejList] == seq) uniform |= W_NOTLIST;
   const uint64_t ntiles = uniform ? 0 : (n + tileN - 1) / tileN;
   const uint32_t tag = tile_tag(seq);
   int partial = 0;
@@ -1048,6 +1120,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_apply_db(uint64_t n, const Win
   uint32_t uniform = rej[kPending] != 0 ? (uint32_t)W_GATED : 0u;
   if (rej[kRejRange] == seq) uniform |= W_RANGE;
   if (rej[kRejUnsorted] == seq) uniform |= W_UNSORTED;
+  if (rej[kRejList] == seq) uniform |= W_NOTLIST;
   const uint64_t ntiles = uniform ? 0 : (n + tileN - 1) / tileN;
   const uint32_t tag = tile_tag(seq);
   // the first tile's chunks
@@ -2119,12 +2192,19 @@ static psg_store::WinCache* win_entry(psg_store* s, const uint64_t* q, uint64_t 
     e->lean_fail = 0;
     e->ident_ok = 0;
     e->ident_trial = 0;
+    e->copy_gen = 0;
+    e->vl_fail = 0;
+    e->learn_ticket = 0;
   }
   if (e->cap_tiles < ntiles) {
     if (e->win) (void)hipFree(e->win);
     if (e->codes) (void)hipFree(e->codes);
+    if (e->copy) (void)hipFree(e->copy);
     e->win = nullptr;
     e->codes = nullptr;
+    e->copy = nullptr;
+    e->copy_cap = 0;
+    e->copy_gen = 0;
     e->cap_tiles = 0;
     const uint64_t cap = std::max<uint64_t>(ntiles, 64);
     if (hipMalloc(&e->win, cap * sizeof(Win)) != hipSuccess) return nullptr;
@@ -2592,7 +2672,43 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     wc->codes = nullptr;
   }
   const bool coded_ran = mident && coded_on && wc->codes;
-  if (coded_ran) {
+  // the tiles the coded validation sorts as stretch or coded go to the lean
+  // apply (k_tile_apply) while this list's last attempt left no general tile
+  // against this K; f32 values (PSG_RA_LEAN=0: k_resolve_apply<MI>, A/B)
+  static const bool lean_on = [] {
+    const char* e = getenv("PSG_RA_LEAN");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const bool lean = lean_on && coded_ran && DT == PSG_F32 && (op & PSG_PUSH) && wc->lean_fail != s->gen;
+  // A lean Push of a list that equals its verified copy needs no validation
+  // pass against the store: k_list_check compares it with the copy (16 B per
+  // key against 8 / density + 1 of store keys and lane codes) and takes the
+  // tiles' kinds from their windows.  The copy is kept by a learning request
+  // (k_validate_code writes the keys it validates) and holds while K keeps the
+  // generation it was validated against.  PSG_RA_VL=0: never (A/B).
+  static const bool vl_on = [] {
+    const char* e = getenv("PSG_RA_VL");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const bool vl_ok = vl_on && lean && wc->vl_fail != s->gen;
+  if (vl_ok && !wc->copy) {
+    // (no request in flight reads an absent copy)
+    if (hipMalloc(&wc->copy, wc->cap_tiles * 4096 * sizeof(uint64_t)) == hipSuccess) {
+      wc->copy_cap = wc->cap_tiles * 4096;
+      wc->copy_gen = 0;
+    } else {
+      (void)hipGetLastError();
+      wc->copy = nullptr;
+    }
+  }
+  const bool use_vl = vl_ok && wc->copy && wc->copy_cap >= n && wc->copy_gen == s->gen;
+  const bool learn = vl_ok && wc->copy && wc->copy_cap >= n && !use_vl;
+  if (use_vl) {
+    const unsigned gl = grid_n((n + 3) / 4, kBlock);
+    k_list_check<<<gl, kBlock, 0, st>>>(q, wc->copy, n, win, s->gen, s->reject_dev, seq,
+                                        aligned16(q) && aligned16(wc->copy) ? 1 : 0, tile_words(s, s->ring_next));
+    s->counters[PSG_CTR_LISTS]++;
+  } else if (coded_ran) {
     const unsigned cus = (unsigned)(max_stream_blocks() / 8);
     // PSG_VC_BPC (A/B): blocks per CU in the grid (0: one block per tile)
     static const int vc_bpc = [] {
@@ -2602,7 +2718,7 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
     const unsigned gcode = (unsigned)(vc_bpc > 0 ? std::min<uint64_t>(ntiles, (uint64_t)cus * vc_bpc) : ntiles);
     k_validate_code<<<gcode, 1024, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->key_begin, s->key_end,
                                             s->reject_dev, seq, aligned16(q) ? 1 : 0, tile_words(s, s->ring_next),
-                                            wc->codes);
+                                            wc->codes, learn ? wc->copy : nullptr);
     s->counters[PSG_CTR_CODED]++;
   } else if (nsearch + nval > 0)
     k_validate_windows<<<nsearch + nval, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, tile, nsearch,
@@ -2626,15 +2742,9 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   rec->nt = nt;
   rec->seq = seq;
   rec->tw_ring = rec->ring;  // (the slot the validation above wrote: ring_next then)
-  // the tiles the coded validation sorted as stretch or coded go to the lean
-  // apply (k_tile_apply) while this list's last attempt left no general tile
-  // against this K; f32 values (PSG_RA_LEAN=0: k_resolve_apply<MI>, A/B)
-  static const bool lean_on = [] {
-    const char* e = getenv("PSG_RA_LEAN");
-    return e ? atoi(e) != 0 : true;
-  }();
-  const bool lean = lean_on && coded_ran && DT == PSG_F32 && (op & PSG_PUSH) && wc->lean_fail != s->gen;
   rec->lean = lean ? 1 : 0;
+  rec->vl = use_vl ? 1 : (learn ? 2 : 0);
+  if (learn) wc->learn_ticket = rec->ticket;
   s->counters[ident ? PSG_CTR_IDENT : PSG_CTR_FUSED]++;
   if (lean) {
     s->counters[PSG_CTR_LEAN]++;
@@ -2743,6 +2853,31 @@ template <int DT>
 static int finish(psg_store* s, const InflightReq& r, uint32_t f) {
   psg_store::WinCache& wc = s->wc[r.wc];
   end_ident(s, r, !(f & (W_NOTIDENT | W_RANGE)));
+  const bool mine = wc.q == r.q && wc.n == r.n;
+  if (f & W_NOTLIST) {
+    // not its list's verified copy after all (the caller rewrote the keys): it
+    // wrote nothing.  No verified-copy attempt on this list until K changes;
+    // the request runs again with the full validation, to completion (kPending,
+    // which its word raised, is cleared first so it is not gated).
+    if (mine) {
+      wc.copy_gen = 0;
+      wc.vl_fail = s->gen;
+    }
+    s->counters[PSG_CTR_NOTLIST]++;
+    PSG_HIP(hipMemsetAsync(s->reject_dev + kPending, 0, sizeof(int), r.stream));
+    InflightReq r2;
+    PSG_TRY(launch_fused<DT>(s, r.op, r.q, r.n, r.vals, r.out, r.stream, &r2, r.want_land != 0));
+    PSG_REQUIRE(r2.vl != 1, PSG_ERR_HIP, "SORTED store: verified-copy request replayed as one");
+    s->inflight.push_back(r2);
+    int rc2 = PSG_OK;
+    const int rc = reap_t<DT>(s, r2.ticket, r2.ticket, &rc2);
+    return rc != PSG_OK ? rc : rc2;
+  }
+  // a learning request that completed with every tile served lean: its copy of
+  // the list is now the verified copy for this K (the last learner's only)
+  if (r.vl == 2 && mine && wc.learn_ticket == r.ticket &&
+      !(f & (W_RANGE | W_UNSORTED | W_MISSING | W_WINMISS | W_PARTIAL | W_NOTIDENT)))
+    wc.copy_gen = s->gen;
   if (f & W_NOTIDENT) {
     // not an identity request after all: it wrote nothing to the store (a
     // Pull, only its reply).  No identity attempt on this key list until K
@@ -2882,7 +3017,7 @@ static int reap_t(psg_store* s, uint64_t upto, uint64_t own, int* own_rc) {
       replay(r);
       continue;
     }
-    const bool follow = !(f & W_RANGE) && (f & (W_MISSING | W_UNSORTED | W_NOTIDENT));
+    const bool follow = !(f & W_RANGE) && (f & (W_MISSING | W_UNSORTED | W_NOTIDENT | W_NOTLIST));
     if (!follow) {
       note(s, r.ticket, finish<DT>(s, r, f), own, own_rc);
       continue;
@@ -3422,6 +3557,7 @@ int psg_store_destroy(psg_store* s) {
   for (auto& c : s->wc) {
     if (c.win) (void)hipFree(c.win);
     if (c.codes) (void)hipFree(c.codes);
+    if (c.copy) (void)hipFree(c.copy);
   }
   delete s;
   return PSG_OK;

@@ -49,7 +49,7 @@ EXPORTS = [
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
     "psg_comm_bucket_plan", "psg_comm_keyed_plan", "psg_comm_sync", "psg_comm_abort",
-    "psg_adam_create", "psg_adam_destroy", "psg_lr_apply", "psg_lr_apply_sum",
+    "psg_adam_create", "psg_adam_destroy", "psg_lr_apply", "psg_lr_apply_sum", "psg_lr_mix_copy",
     "psg_comm_lr_push", "psg_xgmi_lr_push",
     "psg_ipc_handle_bytes", "psg_ipc_export", "psg_ipc_export_range", "psg_ipc_open", "psg_ipc_close", "psg_xgmi_create",
     "psg_xgmi_destroy", "psg_xgmi_push", "psg_xgmi_pull", "psg_xgmi_push_range",
@@ -151,6 +151,7 @@ def lib() -> C.CDLL:
             "psg_adam_destroy": ([vp], i32),
             "psg_lr_apply": ([vp, vp, u64, f32, vp, i32, vp], i32),
             "psg_lr_apply_sum": ([vp, C.POINTER(vp), i32, i32, u64, f32, vp, i32, vp], i32),
+            "psg_lr_mix_copy": ([vp, C.POINTER(vp), i32, u64, vp, vp], i32),
             "psg_comm_lr_push": ([vp, vp, vp, u64, f32, vp, i32, vp, vp], i32),
             "psg_xgmi_lr_push": ([vp, vp, u64, f32, vp, i32, vp], i32),
             "psg_ipc_handle_bytes": ([], i32), "psg_ipc_export": ([vp, vp], i32),
@@ -382,11 +383,11 @@ class Store:
 
     def counters(self) -> dict:
         """How the store served its keyed requests (psg_store_counters)."""
-        c = (C.c_uint64 * 11)()
-        _call("psg_store_counters", self.h, c, 11)
+        c = (C.c_uint64 * 13)()
+        _call("psg_store_counters", self.h, c, 13)
         return {"fused": c[0], "ident": c[1], "notident": c[2], "ordered": c[3], "runs": c[4],
                 "run_frames": c[5], "coded": c[6], "lean": c[7], "lean_partial": c[8],
-                "strided_runs": c[9], "strided_frames": c[10]}
+                "strided_runs": c[9], "strided_frames": c[10], "lists": c[11], "notlist": c[12]}
 
     def handle(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> None:
         _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,
@@ -617,6 +618,13 @@ def lr_apply_sum(weights: Store, grads, n: int, lr: float, adam: Adam | None, it
     arr = (C.c_void_p * max(len(grads), 1))(*[_ptr(g) for g in grads])
     _call("psg_lr_apply_sum", weights.h, arr, len(grads), int(from_zero), n, lr,
           adam.h if adam else None, iteration, _s(stream))
+
+
+def lr_mix_copy(weights: Store, grads, n: int, adam: Adam, stream=None) -> None:
+    """psg_lr_mix_copy: the Adam apply's loads and stores with a copy's arithmetic
+    (measurement only: it scribbles on the weights and moments)."""
+    arr = (C.c_void_p * max(len(grads), 1))(*[_ptr(g) for g in grads])
+    _call("psg_lr_mix_copy", weights.h, arr, len(grads), n, adam.h, _s(stream))
 
 
 # ---- one-shot xGMI exchange ----------------------------------------------------------

@@ -18,6 +18,9 @@
 #   lrb      the bench line of the LR BSP round (bench.py --workload lr) + its rocprof stats
 #   dropin:N:MODE:LAYOUT  the drop-in API line at ns = nw = N (MODE threads|procs,
 #            LAYOUT 0 the benchmark's interleaved keys, 1 one shared list)
+#   strided  kernel stats of strided runs alone (4 / 8 requests, Push / Pull)
+#   pmcstrided  PMC traffic of the 4-request strided Push and Pull passes
+#   pmccalib the gfx950 PMC calibration passes (tools/_bin/probe_pmc_shapes)
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
 #            (tools/pmc_targets.py, two passes each)
 set -u
@@ -97,6 +100,46 @@ for st in "$@"; do
           md=""; [ "$dm" = procs ] && md="-procs"
           step 240 rocprofv3 --kernel-trace --stats -d gpurun_out/dprof_$tag -o run --output-format csv -- tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dprof_$tag.log 2>&1; echo "$st rc=$?"; grep '"rank": 0' gpurun_out/dprof_$tag.log | cut -c1-300
           f=$(find gpurun_out/dprof_$tag -name "*kernel_stats.csv" | head -1); cut -c1-180 "$f" | head -12 ;;
+    strided)
+          # the strided run's kernels alone (tools/pmc_targets.py): kernel stats
+          # and PMC traffic of a 4- and an 8-request run, Push and Pull
+          for t in strided4push strided4pull strided8push strided8pull; do
+            rm -rf gpurun_out/prof_$t
+            step 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$t -o run --output-format csv -- python3 tools/pmc_targets.py $t 20 > gpurun_out/prof_$t.log 2>&1; echo "$t rc=$?"
+            python3 - "$t" <<'PY'
+import csv, sys
+t = sys.argv[1]
+for r in csv.DictReader(open(f"gpurun_out/prof_{t}/run_kernel_stats.csv")):
+    n = r["Name"]
+    if "k_run" in n:
+        avg = float(r["AverageNs"]) / 1e3
+        per = 16 if "k_run_pass<0, 0>" in n else (12 if "k_run_pass<0, 1>" in n else (24 if "k_run_pass<0, 2>" in n else 0))
+        frac = (per * 10e6 / (avg * 1e-6) / 8e12) if per else 0
+        print(f"  {n[:60]:60s} calls {r['Calls']:>4} avg {avg:8.1f} us  {per} B/key -> {frac:.3f} of 8 TB/s")
+PY
+          done ;;
+    pmcstrided)
+          bash tools/pmc.sh gpurun_out/pmc_strided s4push 'k_run_pass<0, 0>|k_run_pass<0, 1>' 10000000 28 python3 tools/pmc_targets.py strided4push 10 && cat gpurun_out/pmc_strided/s4push.json
+          bash tools/pmc.sh gpurun_out/pmc_strided s4pull 'k_run_pass<0, 2>' 10000000 24 python3 tools/pmc_targets.py strided4pull 10 && cat gpurun_out/pmc_strided/s4pull.json ;;
+    pmccalib)
+          # the gfx950 FETCH/WRITE calibration per access shape:
+          # four counter passes and a trace over tools/_bin/probe_pmc_shapes
+          out=gpurun_out/pmc_calib; rm -rf "$out"; mkdir -p "$out"; R=$PWD
+          ( cd /tmp && export TMPDIR=/tmp &&
+            timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$out/fetch" -- "$R/tools/_bin/probe_pmc_shapes" 3 &&
+            timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/$out/write" -- "$R/tools/_bin/probe_pmc_shapes" 3 &&
+            timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum --output-format csv -d "$R/$out/rdreq" -- "$R/tools/_bin/probe_pmc_shapes" 3 &&
+            timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$R/$out/wrreq" -- "$R/tools/_bin/probe_pmc_shapes" 3 &&
+            timeout -s KILL 90 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$out/trace" -- "$R/tools/_bin/probe_pmc_shapes" 3 ) > "$out.log" 2>&1
+          rc=$?; echo "pmccalib rc=$rc"; stop_on_crash $rc
+          python3 tools/pmc_calib.py "$out" "$out/calibration.json" ;;
+    dstage:*)
+          # dstage:N:mode:layout:gather — kv_bench_dropin with the host stage times
+          # (PS_STAGE_TIMES=1), summarised per stage (tools/stage_summary.py)
+          IFS=: read -r _ dn dm dl dg <<< "$st"; tag="n${dn}_${dm}_l${dl}_g${dg:-0}"
+          md=""; [ "$dm" = procs ] && md="-procs"
+          PS_RUN_GATHER_US=${dg:-0} PS_STAGE_TIMES=1 step 200 tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dstage_$tag.log 2>&1; echo "$st rc=$?"; grep '"rank": 0' gpurun_out/dstage_$tag.log | cut -c1-300
+          python3 tools/stage_summary.py gpurun_out/dstage_$tag.log 40 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""The gfx950 HBM counter calibration table from tools/r5_pmc_calib.sh's passes
-over tools/probe_pmc_shapes.
+"""The gfx950 HBM counter calibration table from the `pmccalib` passes of
+tools/gpu_run.sh over tools/_bin/probe_pmc_shapes (make -C tools).
 
 usage: pmc_calib.py PASS_DIR OUT_JSON
 

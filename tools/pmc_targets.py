@@ -12,6 +12,13 @@ launch).
   frames_keyed8/4 a run of 8 (4) Pushes of one 10 M-key list = the SORTED store (16 + 12k B / key)
   frames_cached8/4 a run of 8 (4) Pushes on a cached stretch of slots (8 + 4k B / key)
 
+  strided4push / strided4pull / strided8push / strided8pull
+                  a run of P = 4 (8) requests on the reference benchmark's
+                  interleaved lists (kMaxKey/num*i + r), 10 M store keys in all —
+                  one server's share of the drop-in line at ns = nw = P:
+                  k_run_pass check + apply (28 B / key) / the checked Pull
+                  pass (24 B / key), psg_store_run
+
 usage: pmc_targets.py TARGET [LAUNCHES]
 """
 import os
@@ -89,6 +96,27 @@ elif what in ("frames_cached8", "frames_cached4"):
         v.fill_synth(n, psg.F32, 7 + j, 0, 0.0, 100.0, s)
     for _ in range(reps):
         st.push_slots_frames(None, vs, n, first=first, stream=s)
+elif what.startswith("strided"):
+    import numpy as np
+    P = int(what[7])
+    op = psg.PUSH if what.endswith("push") else psg.PULL
+    n = 10_000_000 // P
+    step = np.uint64(((1 << 64) - 1) // n)
+    lists = [np.arange(n, dtype=np.uint64) * step + np.uint64(r) for r in range(P)]
+    st = psg.Store(psg.SORTED, psg.F32, 0, (1 << 64) - 1, 0)
+    dks = [psg.DeviceBuffer.from_numpy(l, s) for l in lists]
+    vs = [psg.DeviceBuffer(n * 4) for _ in range(P)]
+    outs = [psg.DeviceBuffer(n * 4) for _ in range(P)]
+    for j, v in enumerate(vs):
+        v.fill_synth(n, psg.F32, 7 + j, 0, 0.0, 100.0, s)
+    for j in range(P):
+        st.handle(psg.PUSH, dks[j], vs[j], None, n, stream=s)
+    order = list(range(P))[::-1]
+    for _ in range(reps):
+        served = st.run([op] * P, [dks[j] for j in order], [n] * P,
+                        [vs[j] if op == psg.PUSH else None for j in order],
+                        [outs[j] if op == psg.PULL else None for j in order], stream=s)
+        assert served == psg.RUN_STRIDED, served
 else:
     raise SystemExit(f"unknown target {what}")
 s.sync()

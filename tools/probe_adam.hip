@@ -10,7 +10,7 @@
 // Also the plain streams of the same bytes: rmw (the moment array read and
 // written back, 16 B per lane, grid-stride) and copy (1 GB read, 1 GB written).
 // Prints ms and the fraction of 8 TB/s at the algorithmic bytes.
-// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/probe_adam.hip -o tools/_probe_adam
+// Build: make -C tools  (tools/_bin/probe_adam)
 #include <hip/hip_runtime.h>
 
 #include <cmath>

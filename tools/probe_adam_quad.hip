@@ -14,7 +14,7 @@
 // Plus, in the same process, a 16-B copy of the same total bytes (28 B read and
 // 28 B written per feature, two 1.9 GB buffers at 64 M), at several shapes:
 // what a plain stream of the apply's byte volume reaches on this box.
-// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/_bin/probe_adam_quad tools/probe_adam_quad.hip
+// Build: make -C tools  (tools/_bin/probe_adam_quad)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

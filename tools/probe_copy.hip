@@ -1,7 +1,7 @@
 // probe_copy.hip — what a 1 GiB float4 copy (read 1 GiB, write 1 GiB: the
 // 256 M-float Pull's exact traffic) reaches on this MI355X, by kernel shape,
 // all in one process on the same two buffers, interleaved rounds.
-//   hipcc --offload-arch=gfx950 -O3 -o /tmp/probe_copy tools/probe_copy.hip
+//   make -C tools  (tools/_bin/probe_copy)
 //   probe_copy [MiB] [rounds]
 // Variants: grid-stride with U vectors per lane in flight and B blocks per CU,
 // non-temporal (nt) or default loads / stores, and a chunked form where each

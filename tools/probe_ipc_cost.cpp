@@ -1,7 +1,7 @@
 // probe_ipc_cost.cpp — per-call host cost of the runtime calls on the TCP Van's
 // HBM-frame path (process mode): hipMemGetAddressRange, hipIpcGetMemHandle,
 // hipPointerGetAttribute(BUFFER_ID), hipStreamWriteValue32, hipStreamSynchronize.
-// build: hipcc --offload-arch=gfx950 -O2 tools/probe_ipc_cost.cpp -o tests/_bin/probe_ipc_cost
+// build: make -C tools  (tools/_bin/probe_ipc_cost)
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>

@@ -4,7 +4,7 @@
 // between requests), timed the way bench.py times them: Push then Pull on one
 // stream, an event before, between and after, medians over 30 steps, shapes
 // interleaved over rounds, one process.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/_bin/probe_push_small tools/probe_push_small.hip
+//   make -C tools  (tools/_bin/probe_push_small)
 //   probe_push_small [floats] [rounds]
 #include <hip/hip_runtime.h>
 

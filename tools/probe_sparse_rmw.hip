@@ -7,7 +7,7 @@
 //   vec_load    two 16-B loads of the lane's 8 slots, 4-B stores of the 4
 //   vec_full    two 16-B loads, the 4 slots updated, both vectors stored back
 //               (every byte of every line written: no partially written line)
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/_bin/probe_sparse_rmw tools/probe_sparse_rmw.hip
+// Build: make -C tools  (tools/_bin/probe_sparse_rmw)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
