@@ -1346,7 +1346,7 @@ def run_dropin(args, n_gpus: int) -> dict:
         # runs in one pass (same list / strided) and the requests they held,
         # of N * N * 2 * (warmup + steps) requests in all
         tot = {k: sum(sv.get(k, 0) for sv in servers) for k in
-               ("fused", "ident", "runs", "run_frames", "strided_runs", "strided_frames")}
+               ("fused", "ident", "runs", "run_frames", "strided_runs", "strided_frames", "strided_single")}
         tot["requests"] = N * N * 2 * (args.warmup + args.steps)
         res["server_counters"] = tot
     if not args.no_cpu_baseline:

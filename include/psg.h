@@ -219,7 +219,10 @@ int psg_store_clear(psg_store* s, psg_stream stream);
  * that list after all and ran again with the full validation */
 #define PSG_CTR_LISTS 11
 #define PSG_CTR_NOTLIST 12
-#define PSG_NCOUNTERS 13
+/* requests served on their own as a strided pass (psg_store_run, k = 1: a list
+ * whose place in a learnt interleaved layout the store knows) */
+#define PSG_CTR_STRIDED_SINGLE 13
+#define PSG_NCOUNTERS 14
 int psg_store_counters(psg_store* s, uint64_t* out, int n);
 
 /* One request, KVServerDefaultHandle::operator() (KVApp.h:435-456):
@@ -332,8 +335,11 @@ int psg_store_push_frames(psg_store* s, const uint64_t* const* keys_host, uint64
  * as it found it.  keys[j], vals[j] (Push), outs[j] (Pull): device arrays of
  * ns[j] elements; 1 <= k <= 16.  *served (may be NULL) = PSG_RUN_*.  Returns
  * as psg_store_handle does: every key and value array is no longer read and
- * every Pull's reply is in memory.  PSG_RUNS_STRIDED=0 never tries the
- * strided pass (A/B). */
+ * every Pull's reply is in memory.  k = 1: a request whose list this store
+ * has seen in a strided run (its first key's slot and period known, at this
+ * K generation) takes the strided pass on its own — its phase's slots of the
+ * rows, against the general path's windows and search — else it is
+ * psg_store_handle.  PSG_RUNS_STRIDED=0 never tries the strided pass (A/B). */
 #define PSG_RUN_ONE_BY_ONE 0
 #define PSG_RUN_SAME_LIST 1
 #define PSG_RUN_STRIDED 2

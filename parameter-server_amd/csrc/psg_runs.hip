@@ -23,11 +23,12 @@
 // i.e. 28 B per pushed key and 24 per pulled key — what one identity request
 // moves — for the whole run.
 //
-// One lane per row: the wave's 64 rows make every request's keys, values and
-// replies one contiguous stream (row i of request j is element i of its
-// arrays), and the row's P slots of the store are P contiguous values and keys,
-// read as 16-B vectors when P is a multiple of the vector width.  The phase ->
-// request map is uniform across the block (LDS).
+// One lane per 16-B chunk of the store's values: every wave instruction on the
+// store's keys and values is one contiguous run, and row i of request j is
+// element i of its arrays, so the lanes that share a phase read that
+// request's keys, values and replies as contiguous runs too (P = 4, f32: one
+// lane per row, every request one stream).  The phase -> request map is
+// uniform across the block (LDS).
 //
 // run_classify looks at first keys only (one block, one wave per request); the
 // passes verify every key.  A mismatch anywhere makes the apply write nothing
@@ -182,83 +183,101 @@ __global__ __launch_bounds__(256) void k_run_pass(typename Elem<DT>::T* __restri
   const uint64_t D = sD, rows = srows;
   const uint32_t P = sP;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  // 16-B vectors of the store along a row when every row starts on one
-  const bool vec = (D % V) == 0 && (P % V) == 0;
+  // One lane per 16-B chunk of store values (V slots) over the rows' slots
+  // [D, D + P rows): every wave instruction on the store's keys and values is
+  // one contiguous run, whatever P.  A chunk's slots are consecutive phases,
+  // wrapping into the next row: one division per chunk.
+  const uint64_t end = D + (uint64_t)P * rows;
+  const uint64_t c0 = D / V, c1 = (end + V - 1) / V;
   int mismatch = 0;
-  for (uint64_t row = (uint64_t)blockIdx.x * kBlock + threadIdx.x; row < rows; row += stride) {
-    const uint64_t base = D + (uint64_t)P * row;
-    const uint32_t r = (uint32_t)row;
-    for (uint32_t c0 = 0; c0 < P; c0 += V) {
-      // phases c0 .. c0 + V - 1 of this row (fewer at the end of a row that
-      // is not a multiple of V: the scalar form)
-      if (vec && base + c0 + V <= S) {
-        int ops[V];
-        bool anyop = false, anypush = false;
+  for (uint64_t t = c0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < c1; t += stride) {
+    const uint64_t a0 = t * V;
+    int ph[V], ops[V];
+    uint32_t rw[V];
+    {
+      // the phase and row of the chunk's first slot (slots before D: none)
+      const uint64_t m0 = a0 >= D ? a0 - D : 0;
+      uint32_t r = (uint32_t)(m0 / P);
+      uint32_t p = (uint32_t)(m0 - (uint64_t)r * P);
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-          const int ph = c0 + e;
-          ops[e] = r < sn[ph] ? sop[ph] : 0;
-          anyop = anyop || ops[e];
-          anypush = anypush || (ops[e] & PSG_PUSH);
+      for (int e = 0; e < V; ++e) {
+        const uint64_t a = a0 + e;
+        const bool in = a >= D && a < end;
+        ph[e] = in ? (int)p : 0;
+        rw[e] = r;
+        ops[e] = in && r < sn[p] ? sop[p] : 0;
+        if (a >= D && ++p == P) {
+          p = 0;
+          ++r;
         }
-        if (!anyop) continue;
-        // every load of the chunk first, then the arithmetic, then the writes
-        uint64_t kk[V], qq[V];
-        T x[V];
-        if constexpr (MODE != RUN_APPLY) {
-          const u64x2* kp = reinterpret_cast<const u64x2*>(K + base + c0);
+      }
+    }
+    bool anyop = false, anypush = false;
 #pragma unroll
-          for (int h = 0; h < V / 2; ++h) {
-            const u64x2 t = __builtin_nontemporal_load(kp + h);
-            kk[2 * h] = t[0];
-            kk[2 * h + 1] = t[1];
-          }
+    for (int e = 0; e < V; ++e) {
+      anyop = anyop || ops[e];
+      anypush = anypush || (ops[e] & PSG_PUSH);
+    }
+    if (!anyop) continue;
+    const bool whole = a0 + V <= S;
+    // every load of the chunk first, then the arithmetic, then the writes
+    uint64_t kk[V], qq[V];
+    if constexpr (MODE != RUN_APPLY) {
+      if (whole) {
+        const u64x2* kp = reinterpret_cast<const u64x2*>(K + a0);
 #pragma unroll
-          for (int e = 0; e < V; ++e) qq[e] = ops[e] ? __builtin_nontemporal_load(sq[c0 + e] + r) : 0;
-        }
-        if constexpr (MODE != RUN_CHECK) {
-          typedef T tv __attribute__((ext_vector_type(V)));
-          const tv y = __builtin_bit_cast(tv, *reinterpret_cast<const u32x4*>(store + base + c0));
-          T a[V];
-#pragma unroll
-          for (int e = 0; e < V; ++e) a[e] = (ops[e] & PSG_PUSH) ? __builtin_nontemporal_load(sv[c0 + e] + r) : T(0);
-#pragma unroll
-          for (int e = 0; e < V; ++e) x[e] = (ops[e] & PSG_PUSH) ? E::add1(y[e], a[e]) : y[e];
-        }
-        if constexpr (MODE != RUN_APPLY) {
-#pragma unroll
-          for (int e = 0; e < V; ++e)
-            if (ops[e] && qq[e] != kk[e]) mismatch = 1;
-        }
-        if constexpr (MODE != RUN_CHECK) {
-#pragma unroll
-          for (int e = 0; e < V; ++e)
-            if (ops[e] & PSG_PULL) __builtin_nontemporal_store(x[e], so[c0 + e] + r);
-          if (MODE == RUN_APPLY && anypush) {
-            typedef T tv __attribute__((ext_vector_type(V)));
-            tv y;
-#pragma unroll
-            for (int e = 0; e < V; ++e) y[e] = x[e];
-            // the slots of the row no request of the run holds go back
-            // unchanged: only this stream writes the store
-            *reinterpret_cast<u32x4*>(store + base + c0) = __builtin_bit_cast(u32x4, y);
-          }
+        for (int h = 0; h < V / 2; ++h) {
+          const u64x2 x = __builtin_nontemporal_load(kp + h);
+          kk[2 * h] = x[0];
+          kk[2 * h + 1] = x[1];
         }
       } else {
-        const uint32_t c1 = c0 + V < P ? c0 + V : P;
-        for (uint32_t ph = c0; ph < c1; ++ph) {
-          const int op = r < sn[ph] ? sop[ph] : 0;
-          if (!op) continue;
-          const uint64_t a = base + ph;
-          if constexpr (MODE != RUN_APPLY) {
-            if (sq[ph][r] != K[a]) mismatch = 1;
-          }
-          if constexpr (MODE != RUN_CHECK) {
-            T x = store[a];
-            if (op & PSG_PUSH) x = E::add1(x, sv[ph][r]);
-            if (op & PSG_PULL) so[ph][r] = x;
-            if (MODE == RUN_APPLY && (op & PSG_PUSH)) store[a] = x;
-          }
+#pragma unroll
+        for (int e = 0; e < V; ++e) kk[e] = ops[e] ? K[a0 + e] : 0;
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) qq[e] = ops[e] ? __builtin_nontemporal_load(sq[ph[e]] + rw[e]) : 0;
+    }
+    T x[V];
+    if constexpr (MODE != RUN_CHECK) {
+      T y[V];
+      if (whole) {
+        typedef T tv __attribute__((ext_vector_type(V)));
+        const tv w = __builtin_bit_cast(tv, *reinterpret_cast<const u32x4*>(store + a0));
+#pragma unroll
+        for (int e = 0; e < V; ++e) y[e] = w[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) y[e] = ops[e] ? store[a0 + e] : T(0);
+      }
+      T a[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) a[e] = (ops[e] & PSG_PUSH) ? __builtin_nontemporal_load(sv[ph[e]] + rw[e]) : T(0);
+#pragma unroll
+      for (int e = 0; e < V; ++e) x[e] = (ops[e] & PSG_PUSH) ? E::add1(y[e], a[e]) : y[e];
+    }
+    if constexpr (MODE != RUN_APPLY) {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (ops[e] && qq[e] != kk[e]) mismatch = 1;
+    }
+    if constexpr (MODE != RUN_CHECK) {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (ops[e] & PSG_PULL) __builtin_nontemporal_store(x[e], so[ph[e]] + rw[e]);
+      if (MODE == RUN_APPLY && anypush) {
+        if (whole) {
+          typedef T tv __attribute__((ext_vector_type(V)));
+          tv w;
+#pragma unroll
+          for (int e = 0; e < V; ++e) w[e] = x[e];
+          // the chunk's slots no request of the run holds go back unchanged:
+          // only this stream writes the store
+          *reinterpret_cast<u32x4*>(store + a0) = __builtin_bit_cast(u32x4, w);
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if (ops[e] & PSG_PUSH) store[a0 + e] = x[e];
         }
       }
     }

@@ -25,6 +25,7 @@ namespace psg {
 constexpr int kMaxTargets = 64;
 struct Targets {
   uint64_t v[kMaxTargets];
+  uint64_t hint[kMaxTargets];  // the bound this key array had last time (UINT64_MAX: none)
 };
 
 // pos_sys (may be NULL): the same bound into pinned host memory, tagged —
@@ -38,6 +39,22 @@ __global__ __launch_bounds__(256) void k_bounds(const uint64_t* __restrict__ key
                                                 uint64_t* __restrict__ pos_sys, uint64_t tag) {
   const uint64_t target = t.v[blockIdx.x];
   uint64_t lo = 0, hi = n;  // the answer (first index with keys >= target) is in [lo, hi]
+  // The bound this array had at its last slice (a worker slices the same key
+  // array request after request): confirmed by the two keys around it — one
+  // round of loads instead of the search's three under the load of the
+  // servers' kernels.  (The keys are sorted, as the slicer requires.)
+  const uint64_t h = t.hint[blockIdx.x];
+  if (h <= n) {
+    __shared__ int s_ok[2];
+    if (threadIdx.x < 2) {
+      const uint64_t i = h - 1 + threadIdx.x;  // keys[h - 1] < target <= keys[h]
+      s_ok[threadIdx.x] = threadIdx.x == 0 ? (h == 0 || keys[i] < target) : (h == n || keys[i] >= target);
+    }
+    __syncthreads();
+    if (s_ok[0] && s_ok[1]) {
+      lo = hi = h;
+    }
+  }
   while (hi - lo > (uint64_t)kBlock) {
     const uint64_t step = (hi - lo + kBlock - 1) / kBlock;
     const uint64_t p = lo + (uint64_t)threadIdx.x * step;
@@ -54,7 +71,7 @@ __global__ __launch_bounds__(256) void k_bounds(const uint64_t* __restrict__ key
   }
   const uint64_t p = lo + threadIdx.x;
   const int pred = (p < hi) && (keys[p] < target);
-  const uint64_t c = (uint64_t)__syncthreads_count(pred);
+  const uint64_t c = lo == hi ? 0 : (uint64_t)__syncthreads_count(pred);
   if (threadIdx.x == 0) {
     pos[blockIdx.x] = lo + c;
     if (pos_sys)
@@ -121,6 +138,16 @@ struct SliceScratch {
   uint64_t* pos_map_dev = nullptr;
   uint64_t tag = 0;
   int cap = 0;
+  // the bounds of the last key arrays sliced (the next slice's hints)
+  struct Last {
+    const uint64_t* keys = nullptr;
+    uint64_t n = 0;
+    int nb = 0;
+    uint64_t begin0 = 0;
+    std::vector<uint64_t> pos;
+    uint64_t use = 0;
+  } last[8];
+  uint64_t clock = 0;
 };
 static thread_local std::map<int, SliceScratch> t_slice_scratch;
 
@@ -205,12 +232,17 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
   sc->tag = (sc->tag + 1) & ((1ull << (64 - kPosBits)) - 1);
   if (sc->tag == 0) sc->tag = 1;
   const uint64_t tag = sc->tag;
+  // hints: this array's bounds at its last slice against the same ranges
+  SliceScratch::Last* hint = nullptr;
+  for (auto& l : sc->last)
+    if (l.keys == keys && l.n == n && l.nb == nb && l.begin0 == begins_host[0]) hint = &l;
   for (int b0 = 0; b0 < nb; b0 += kMaxTargets) {
     Targets t;
     const int cnt = std::min(kMaxTargets, nb - b0);
     for (int j = 0; j < cnt; ++j) {
       const int b = b0 + j;
       t.v[j] = b == 0 ? begins_host[0] : ends_host[b - 1];
+      t.hint[j] = hint ? hint->pos[b] : UINT64_MAX;
     }
     k_bounds<<<cnt, kBlock, 0, st>>>(keys, n, t, pos_dev + b0, tagged ? sc->pos_map_dev + b0 : nullptr, tag);
   }
@@ -240,6 +272,22 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
   }
   if (e != hipSuccess) {
     rc = hip_fail(e, "psg_slice bounds", __FILE__, __LINE__);
+  } else {
+    // remember these bounds for the next slice of this array (LRU of 8)
+    SliceScratch::Last* l = hint;
+    if (!l) {
+      l = &sc->last[0];
+      for (auto& c : sc->last)
+        if (c.use < l->use) l = &c;
+    }
+    l->keys = keys;
+    l->n = n;
+    l->nb = nb;
+    l->begin0 = begins_host[0];
+    l->pos.assign(key_pos_host, key_pos_host + nb);
+    l->use = ++sc->clock;
+  }
+  if (rc != PSG_OK) {
   } else if (key_pos_host[num_servers] != n) {
     // a key at or above the last range's end: CHECK_EQ(pos[n], send.keys.size()),
     // KVApp.h:544.  (Keys below ranges[0].begin are dropped, as in the

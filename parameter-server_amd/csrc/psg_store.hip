@@ -3350,7 +3350,10 @@ static int run_sorted(psg_store* s, int k, const int* ops, const uint64_t* const
     max_n = ns[j] > max_n ? ns[j] : max_n;
     if (pl < 0 && ns[j] >= 2) pl = j;
   }
-  bool try_same = all_push && same_n && ns[0] <= s->size;
+  // (a request on its own is a strided pass only when the host knows its
+  // list's place: a single phase of a learnt layout, which moves 8 P + 8 P + 12
+  // B per key of lines against the general path's windows and search)
+  bool try_same = k > 1 && all_push && same_n && ns[0] <= s->size;
   bool try_strided = strided_on() && pl >= 0 && total <= s->size;
   // a run with Pulls that was not strided at this K generation: the next few
   // are served one by one without a try (a run of Pushes always tries: the
@@ -3378,6 +3381,7 @@ static int run_sorted(psg_store* s, int k, const int* ops, const uint64_t* const
   RunDesc given;
   memset(&given, 0, sizeof(given));
   const bool cached = !try_same && try_strided && run_from_cache(s, k, keys, ns, &given);
+  if (k == 1 && !cached) return run_one_by_one(s, k, ops, keys, ns, vals, outs, st);
   RunDesc* desc = cached ? nullptr : static_cast<RunDesc*>(s->run_desc);
   uint64_t* base = reinterpret_cast<uint64_t*>(s->reject_dev + kFramesBase);
   int* rej = s->reject_dev + kRejIdent;
@@ -3409,8 +3413,12 @@ static int run_sorted(psg_store* s, int k, const int* ops, const uint64_t* const
   }
   if (try_strided && !s->flags_host[F_WINMISS]) {
     *served = PSG_RUN_STRIDED;
-    s->counters[PSG_CTR_STRIDED_RUNS]++;
-    s->counters[PSG_CTR_STRIDED_FRAMES] += (uint64_t)k;
+    if (k == 1) {
+      s->counters[PSG_CTR_STRIDED_SINGLE]++;
+    } else {
+      s->counters[PSG_CTR_STRIDED_RUNS]++;
+      s->counters[PSG_CTR_STRIDED_FRAMES] += (uint64_t)k;
+    }
     if (!cached) run_remember(s, k, keys, ns, *s->run_seen);
     return PSG_OK;
   }
@@ -3794,12 +3802,12 @@ int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* ke
   int sv = PSG_RUN_ONE_BY_ONE;
   bool empty = false;
   for (int j = 0; j < k; ++j) empty = empty || ns[j] == 0;
-  if (k == 1 || empty || s->kind != PSG_STORE_SORTED || !sorted_fused() || s->size == 0) {
+  if (empty || s->kind != PSG_STORE_SORTED || !sorted_fused() || s->size == 0) {
     PSG_TRY(run_one_by_one(s, k, ops, keys, ns, vals, outs, st));
   } else {
     PSG_TRY(run_sorted(s, k, ops, keys, ns, vals, outs, st, &sv));
   }
-  s->run_last = sv;
+  if (k > 1) s->run_last = sv;
   if (served) *served = sv;
   return PSG_OK;
 }

@@ -933,7 +933,10 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       if (next.meta.direct_reply) it.out = next.data[next.data.size() - 1];
       items.push_back(std::move(it));
     }
-    if (items.size() > 1) {
+    // (a plain request on its own goes to the run handle too: the store
+    // serves it as a strided pass when it knows its list's place in a learnt
+    // interleaved layout, else as one request)
+    if (items.size() > 1 || detail::MixedRunsOn()) {
       direct_out_ = SVector<Value>();
       for (size_t j = 0; j < items.size(); ++j)
         detail::TraceRequest(PostOffice::Get()->my_id(), items[j].meta, items[j].data.keys.size(), items.size(), j);

@@ -383,11 +383,11 @@ class Store:
 
     def counters(self) -> dict:
         """How the store served its keyed requests (psg_store_counters)."""
-        c = (C.c_uint64 * 13)()
-        _call("psg_store_counters", self.h, c, 13)
+        c = (C.c_uint64 * 14)()
+        _call("psg_store_counters", self.h, c, 14)
         return {"fused": c[0], "ident": c[1], "notident": c[2], "ordered": c[3], "runs": c[4],
                 "run_frames": c[5], "coded": c[6], "lean": c[7], "lean_partial": c[8],
-                "strided_runs": c[9], "strided_frames": c[10], "lists": c[11], "notlist": c[12]}
+                "strided_runs": c[9], "strided_frames": c[10], "lists": c[11], "notlist": c[12], "strided_single": c[13]}
 
     def handle(self, flags: int, keys, vals, out, n: int, first_key: int = 0, stream=None) -> None:
         _call("psg_store_handle", self.h, flags, _ptr(keys), first_key, _ptr(vals), _ptr(out), n,

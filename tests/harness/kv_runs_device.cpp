@@ -50,10 +50,11 @@ int main(int argc, char* argv[]) {
       uint64_t c[PSG_NCOUNTERS] = {};
       if (h.store()) device::Check(psg_store_counters(h.store(), c, PSG_NCOUNTERS), "psg_store_counters");
       std::printf("{\"server\": %d, \"fused\": %llu, \"ident\": %llu, \"notident\": %llu, \"ordered\": %llu, "
-                  "\"runs\": %llu, \"run_frames\": %llu, \"strided_runs\": %llu, \"strided_frames\": %llu}\n",
+                  "\"runs\": %llu, \"run_frames\": %llu, \"strided_runs\": %llu, \"strided_frames\": %llu, \"strided_single\": %llu}\n",
                   id, (unsigned long long)c[0], (unsigned long long)c[1], (unsigned long long)c[2],
                   (unsigned long long)c[3], (unsigned long long)c[4], (unsigned long long)c[5],
-                  (unsigned long long)c[PSG_CTR_STRIDED_RUNS], (unsigned long long)c[PSG_CTR_STRIDED_FRAMES]);
+                  (unsigned long long)c[PSG_CTR_STRIDED_RUNS], (unsigned long long)c[PSG_CTR_STRIDED_FRAMES],
+                  (unsigned long long)c[PSG_CTR_STRIDED_SINGLE]);
       std::fflush(stdout);
       delete server;
     });

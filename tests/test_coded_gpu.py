@@ -108,7 +108,9 @@ def test_random_subset_lists_take_coded_tiles(dtype, density):
     k = subset(rng, univ, density)
     run_sequence(st, orc, dtype, k, 500)
     c = st.counters()
-    assert c["coded"] >= 4, c
+    # (f32: once a Push of the list has been validated in full and served
+    # lean, its verified copy validates the later ones: k_list_check)
+    assert c["coded"] + c["lists"] >= 4, c
     assert c["ident"] == 0 or c["notident"] >= 1, c
 
 

@@ -854,6 +854,32 @@ def test_slice_vs_oracle_large(n, ns):
     np.testing.assert_array_equal(vp2, ovp2)
 
 
+@pytest.mark.parametrize("ns", [2, 4, 8])
+def test_slice_of_a_rewritten_array_is_searched_again(ns):
+    """The slicer confirms the bounds an array had at its last slice in one
+    round (psg_slice's hints); an array rewritten in place — bounds moved by
+    a few keys, by many, or not at all — still slices as the oracle does."""
+    rng = np.random.default_rng(ns)
+    n = 200_000
+    b, e = psg.server_ranges(ns)
+    dk = psg.DeviceBuffer(n * 8)
+    for trial in range(6):
+        if trial % 3 == 2:
+            keys = np.sort(rng.integers(0, KMAX, n, dtype=np.uint64))  # everything moves
+        elif trial % 3 == 1:
+            keys = keys.copy()
+            keys[:7] = np.sort(rng.integers(0, int(b[1]) if ns > 1 else 1 << 60, 7, dtype=np.uint64))
+            keys = np.sort(keys)  # a few keys move across the first bound
+        else:
+            keys = np.sort(rng.integers(0, KMAX, n, dtype=np.uint64)) if trial == 0 else keys
+        dk.upload(keys)
+        psg.device_sync()
+        for _ in range(2):  # the second slice of the same contents takes the hints
+            kp, _ = psg.slice_keys(dk, n, b, e)
+            okp, _ = oracle.slice_keys(keys, b, e)
+            np.testing.assert_array_equal(kp, okp, err_msg=f"trial {trial}")
+
+
 def test_slice_rejects_key_past_last_range():
     b, e = psg.server_ranges(4)
     with pytest.raises(psg.PsgError):

@@ -227,3 +227,21 @@ def test_a_rejected_request_stops_the_run():
         st.run([PUSH, PUSH], [dev(lists[0]), dev(bad)], [len(lists[0]), len(bad)], [dev(v0), dev(v1)], [None, None])
     orc.handle(oracle.PUSH, lists[0], v0, len(lists[0]))
     same_store(st, orc, dtype)
+
+
+def test_a_learnt_list_on_its_own_takes_the_strided_pass():
+    """After a strided run, a request of one of its lists on its own (the
+    first of a step to reach its server) is a strided pass too — its phase's
+    slots of the rows — bit for bit the request; a list the store has not
+    seen in a strided run is served as one request."""
+    dtype = psg.F32
+    P = 4
+    lists, extra = layout(40000, P, head=2)
+    st, orc = populated(dtype, lists, extra, 90)
+    assert run_both(st, orc, dtype, [(PUSH, lists[r]) for r in (1, 3, 0, 2)], 900) == psg.RUN_STRIDED
+    for j, (op, r) in enumerate([(PUSH, 2), (PULL, 0), (PUSH | PULL, 3), (PULL, 2)]):
+        assert run_both(st, orc, dtype, [(op, lists[r])], 910 + 10 * j) == psg.RUN_STRIDED
+    assert run_both(st, orc, dtype, [(PUSH, extra[0])], 990) == psg.RUN_ONE_BY_ONE
+    same_store(st, orc, dtype)
+    c = st.counters()
+    assert c["strided_single"] == 4 and c["strided_runs"] == 1, c
