@@ -1080,6 +1080,15 @@ def run(backend, args, rank: int, world: int, group=None) -> dict | None:
                      "key, 16 B/key — is the whole validation, then values only, 12 B/key; "
                      "requests in flight, each reporting completion and flags in one "
                      "kernel-written word; one server, so no slicer pass)")
+        elif paths.get("lists", 0) > paths.get("coded", 0):  # most Pushes took the verified copy
+            kname = ("SORTED-store Push: k_list_check + k_tile_apply_db "
+                     "(the list's verified copy: the request keys compared with the copy a "
+                     "learning Push of this list kept — its first lean Push at this K, "
+                     "validated in full by k_validate_code — 16 B/key, no store-key lines; "
+                     "tile kinds from the cached windows; then the lean apply from the lane "
+                     "codes; a list that differs from its copy writes nothing and is "
+                     "validated in full; requests in flight, each reporting completion and "
+                     "flags in one kernel-written word; one server, so no slicer pass)")
         elif paths.get("coded", 0) == 0:
             kname = ("SORTED-store Push: k_validate_windows + k_resolve_apply "
                      "(whole-request validation before any write; each tile searches "

@@ -120,6 +120,12 @@ int psg_memset(void* dptr, int value, size_t bytes, psg_stream stream);
 int psg_copy(void* dst, const void* src, uint64_t bytes, int unroll, int blocks_per_cu, psg_stream stream);
 
 int psg_stream_create(psg_stream* stream);
+/* A stream of high priority (priority != 0: the device's greatest,
+ * hipStreamCreateWithPriority) or of the default one.  A worker's small
+ * kernels (the slicer, the merge) go on one, so that a server's long store
+ * kernels sharing the process's hardware queues do not hold them back (no
+ * reference counterpart: the reference slices on the host). */
+int psg_stream_create_priority(psg_stream* stream, int priority);
 int psg_stream_destroy(psg_stream stream);
 int psg_stream_sync(psg_stream stream);
 int psg_event_create(psg_event* ev);

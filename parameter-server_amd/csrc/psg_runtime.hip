@@ -280,6 +280,15 @@ int psg_stream_create(psg_stream* stream) {
   *stream = (psg_stream)s;
   return PSG_OK;
 }
+int psg_stream_create_priority(psg_stream* stream, int priority) {
+  PSG_REQUIRE(stream, PSG_ERR_INVALID, "psg_stream_create_priority: null out");
+  int least = 0, greatest = 0;
+  PSG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  hipStream_t s;
+  PSG_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority ? greatest : least));
+  *stream = (psg_stream)s;
+  return PSG_OK;
+}
 int psg_stream_destroy(psg_stream stream) {
   if (stream) PSG_HIP(hipStreamDestroy((hipStream_t)stream));
   return PSG_OK;

@@ -2155,13 +2155,13 @@ static int insert_missing(psg_store* s, const uint64_t* q, uint64_t n, hipStream
 // 1024).  The tile is 4 keys per lane, so a larger block leaves fewer windows
 // to search (10 M keys: k_tile_windows 11.2 -> 8.8 us from 256 to 512; keyed
 // Push+Pull 606 / 660 / 675 GB/s at 256 / 512 / 1024).
-// A request sparse in the store (the store holds at least 1.5x as many keys
-// as the request asks for — every other key of a larger store, an LR
-// minibatch) gets 256-thread blocks instead: its tiles' windows span more
-// store keys than they have keys, and smaller windows let 8 blocks per CU
-// stage theirs at once instead of 2 (every 2nd key of a 20 M-key store:
-// keyed Push+Pull 484 against 455-459 GB/s; a request covering its range:
-// 1024 stays ahead, 805 against 790; profiles/r4_ab_ra_block_sparse.txt).
+// A request sparse in the store (the store holds more than twice as many
+// keys as the request asks for — an LR minibatch) gets 256-thread blocks
+// instead: its tiles' windows span more store keys than they have keys, and
+// smaller windows let 8 blocks per CU stage theirs at once instead of 2
+// (round 4, on the general path: every 2nd key of a 20 M-key store, keyed
+// Push+Pull 484 against 455-459 GB/s, profiles/r4_ab_ra_block_sparse.txt;
+// since round 6 a request of at least every other store key keeps 1024, below).
 static int ra_block(const psg_store* s, uint64_t n) {
   static const int env = [] {
     const char* e = getenv("PSG_RA_BLOCK");
@@ -2169,7 +2169,12 @@ static int ra_block(const psg_store* s, uint64_t n) {
     return v == 256 || v == 512 || v == 1024 ? v : 0;
   }();
   if (env) return env;
-  return 2 * s->size >= 3 * n ? 256 : 1024;
+  // at least every other store key: 1024-thread tiles, whose windows (at most
+  // 8192 store keys for 4096 request keys) take coded tiles, the lean apply
+  // and the verified copy — every other key of a 20 M-key store, Push 0.38 ->
+  // 0.51 of HBM, Push+Pull 510 -> 585 GB/s against 256-thread tiles (the Pull
+  // alone 0.45 -> 0.43; profiles/r6_keyed_sparse_block_ab.txt)
+  return s->size > 2 * n ? 256 : 1024;
 }
 
 // The window cache entry for request keys (q, n): the entry last filled for

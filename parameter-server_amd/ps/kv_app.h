@@ -158,12 +158,15 @@ inline bool MixedRunsOn() {
   return on;
 }
 /* PS_RUN_GATHER_US: how long a server waits for the requests of the senders
- * it has heard from lately to join a run (KVServer::OnReceive); 0 (default):
- * a run holds what is queued when it starts. */
+ * it has heard from lately to join a run (KVServer::OnReceive); default 120
+ * (the reference benchmark's layout at ns = nw = 4 on one GPU: 477-487 GB/s
+ * with no wait, 574-609 with 120 us, noisier past it:
+ * profiles/r6_dropin_gather_sweep.txt); 0: a run holds what is queued when it
+ * starts. */
 inline int RunGatherMicros() {
   static const int us = [] {
     const char* e = std::getenv("PS_RUN_GATHER_US");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 120;
   }();
   return us;
 }
@@ -463,6 +466,8 @@ class KVServer : public SimpleApp {
   // target: how many requests one step brings), a ring of 64
   int recent_[64] = {};
   unsigned recent_n_ = 0;
+  int gather_idle_ = 0;  // gather windows in a row that timed out with nothing gained
+  int gather_cool_ = 0;  // requests left to take without a window
   void NoteSender(int sender) { recent_[recent_n_++ & 63] = sender; }
   size_t RecentSenders(int sender) {
     NoteSender(sender);
@@ -912,16 +917,30 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     // reach a server microseconds apart, and a request taken alone costs a
     // whole pass over the store's lines.  The wait ends as soon as the head of
     // the queue is a message that may not join.
-    const int gather_us = detail::RunGatherMicros();
+    // A window that keeps timing out with nothing gained (a sender stopped
+    // sending) is skipped for the next 64 requests.
+    const int gather_us = gather_cool_ > 0 ? 0 : detail::RunGatherMicros();
+    if (gather_cool_ > 0) --gather_cool_;
     const size_t want = gather_us > 0 ? RecentSenders(meta.sender) : 0;
     const auto t_gather = std::chrono::steady_clock::now();
+    bool waited = false;
     Message next;
     while ((int)items.size() < kMaxRun) {
       if (!customer_->TakeQueued(mate, &next)) {
         if (items.size() >= want || customer_->Queued() > 0) break;
-        if (std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(gather_us)) break;
+        if (std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(gather_us)) {
+          if (!waited && ++gather_idle_ >= 4) {
+            gather_idle_ = 0;
+            gather_cool_ = 64;
+          }
+          break;
+        }
         __builtin_ia32_pause();
         continue;
+      }
+      if (items.size() >= 1 && std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(1)) {
+        waited = true;  // a request joined after the wait began
+        gather_idle_ = 0;
       }
       NoteSender(next.meta.sender);
       KVRunItem<Value> it;

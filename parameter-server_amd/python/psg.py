@@ -37,7 +37,8 @@ EXPORTS = [
     "psg_abi_version", "psg_last_error", "psg_device_count", "psg_set_device", "psg_device_pci_bus_id",
     "psg_get_device", "psg_device_sync", "psg_enable_peer_access", "psg_malloc", "psg_free", "psg_host_alloc",
     "psg_host_free", "psg_host_register", "psg_host_unregister", "psg_memcpy",
-    "psg_memset", "psg_copy", "psg_stream_create", "psg_stream_destroy", "psg_stream_sync",
+    "psg_memset", "psg_copy", "psg_stream_create", "psg_stream_create_priority", "psg_stream_destroy",
+    "psg_stream_sync",
     "psg_event_create", "psg_event_create_timing", "psg_event_destroy", "psg_event_record", "psg_event_sync",
     "psg_event_elapsed_ms", "psg_stream_wait_event", "psg_fill_synth", "psg_fill_keys_arith", "psg_checksum",
     "psg_verify_synth_sum",

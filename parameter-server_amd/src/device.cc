@@ -75,7 +75,21 @@ psg_stream ThreadStream() {
   auto it = t_streams.by_dev.find(dev);
   if (it != t_streams.by_dev.end()) return it->second;
   psg_stream s = nullptr;
-  Check(psg_stream_create(&s), "psg_stream_create");
+  // A worker's thread stream is of high priority (PS_WORKER_STREAM_PRIORITY=0:
+  // the default): its kernels are the slicer's bounds and the merges, a few
+  // microseconds each, on every request's critical path, while the servers'
+  // store kernels run for tens — nodes run as threads of one process share
+  // its few hardware queues (GPU_MAX_HW_QUEUES), and a bounds kernel queued
+  // behind a store kernel waits for it.
+  static const bool prio_on = [] {
+    const char* e = std::getenv("PS_WORKER_STREAM_PRIORITY");
+    return !(e && std::atoi(e) == 0);
+  }();
+  PostOffice* po = PostOffice::GetIfBound();
+  if (prio_on && po && po->is_worker())
+    Check(psg_stream_create_priority(&s, 1), "psg_stream_create_priority");
+  else
+    Check(psg_stream_create(&s), "psg_stream_create");
   t_streams.by_dev[dev] = s;
   return s;
 }

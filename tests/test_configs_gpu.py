@@ -173,14 +173,15 @@ def test_dropin_bench_line(n, mode, layout):
 
 
 @pytest.mark.parametrize("env_extra,coded", [({"PSG_BENCH_SUBSET": "0.9"}, True), ({"PSG_BENCH_STRETCHES": "16"}, True),
-                                             ({"PSG_RA_IDENT": "0"}, True), ({"PSG_BENCH_STORE_EXTRA": "1"}, False)])
+                                             ({"PSG_RA_IDENT": "0"}, True), ({"PSG_BENCH_STORE_EXTRA": "1"}, True),
+                                             ({"PSG_BENCH_STORE_EXTRA": "2"}, False)])
 def test_keyed_bench_line_store_layouts(env_extra, coded):
     """bench.py --workload keyed on the store layouts DESIGN §5.1 quotes: a random
     90 % subset of the store, a union of 16 stretches, the general path on the
-    store's own list, every other store key.  Parity holds (the pulled vector
-    on the device, an oracle sample), the coded validation ran where the tiles
-    are 1024-thread ones (psg_store_counters), and the roofline names the
-    kernels that ran."""
+    store's own list, every other / every third store key.  Parity holds (the
+    pulled vector on the device, an oracle sample), the coded validation ran
+    where the tiles are 1024-thread ones — at least every other store key —
+    (psg_store_counters), and the roofline names the kernels that ran."""
     env = dict(os.environ, **env_extra)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "keyed", "--keys", "2000000",
                         "--steps", "6", "--warmup", "3", "--no-cpu-baseline", "--no-probe256"],

@@ -80,16 +80,21 @@ def run_both(st, orc, dtype, reqs, seed):
     k = len(reqs)
     ops, dkeys, ns, dvals, douts, hv = [], [], [], [], [], []
     for j, (op, keys) in enumerate(reqs):
+        # keys: a host array (uploaded for this run), or (host array, device
+        # copy) for a list the caller keeps in HBM from run to run, as a
+        # worker does (the store learns lists by their device pointer)
+        keys, dk = keys if isinstance(keys, tuple) else (keys, dev(keys))
         n = len(keys)
         v = oracle.synth(n, dtype, seed + j, 1, -1.0, 1.0) if op & PUSH else None
         ops.append(op)
-        dkeys.append(dev(keys))
+        dkeys.append(dk)
         ns.append(n)
         dvals.append(dev(v) if v is not None else None)
         douts.append(psg.DeviceBuffer(n * np.dtype(NPT[dtype]).itemsize) if op & PULL else None)
         hv.append(v)
     served = st.run(ops, dkeys, ns, dvals, douts)
     for j, (op, keys) in enumerate(reqs):
+        keys = keys[0] if isinstance(keys, tuple) else keys
         exp = orc.handle(op, keys, hv[j], len(keys))
         if op & PULL:
             got = douts[j].download(NPT[dtype], len(keys))
@@ -238,9 +243,12 @@ def test_a_learnt_list_on_its_own_takes_the_strided_pass():
     P = 4
     lists, extra = layout(40000, P, head=2)
     st, orc = populated(dtype, lists, extra, 90)
-    assert run_both(st, orc, dtype, [(PUSH, lists[r]) for r in (1, 3, 0, 2)], 900) == psg.RUN_STRIDED
+    kept = [(l, dev(l)) for l in lists]
+    assert run_both(st, orc, dtype, [(PUSH, kept[r]) for r in (1, 3, 0, 2)], 900) == psg.RUN_STRIDED
     for j, (op, r) in enumerate([(PUSH, 2), (PULL, 0), (PUSH | PULL, 3), (PULL, 2)]):
-        assert run_both(st, orc, dtype, [(op, lists[r])], 910 + 10 * j) == psg.RUN_STRIDED
+        assert run_both(st, orc, dtype, [(op, kept[r])], 910 + 10 * j) == psg.RUN_STRIDED
+    # the same keys at another device address: not learnt, one request
+    assert run_both(st, orc, dtype, [(PUSH, lists[1])], 980) == psg.RUN_ONE_BY_ONE
     assert run_both(st, orc, dtype, [(PUSH, extra[0])], 990) == psg.RUN_ONE_BY_ONE
     same_store(st, orc, dtype)
     c = st.counters()
