@@ -34,6 +34,8 @@
 // passes verify every key.  A mismatch anywhere makes the apply write nothing
 // (the check pass's word), so the caller (psg_store_run) serves the run request
 // by request from the store it found.
+#include <cstdlib>
+
 #include "psg_internal.h"
 
 namespace psg {
@@ -294,9 +296,15 @@ template <int DT>
 int pass_t(int mode, void* store_vals, const uint64_t* K, uint64_t S, const RunFrames& f, uint64_t max_rows,
            const RunDesc* desc, const RunDesc& given, int* bad, int seq, int* flag, hipStream_t st) {
   using T = typename Elem<DT>::T;
-  // one lane per row, grid-strided past the stream cap
+  // one lane per 16-B chunk, grid-strided past the cap: PSG_RUN_BPC blocks of
+  // 256 per CU (default 8, the streaming grid)
+  static const int bpc = [] {
+    const char* e = getenv("PSG_RUN_BPC");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 32 ? v : 8;
+  }();
   uint64_t b = (max_rows + kBlock - 1) / kBlock;
-  const uint64_t cap = (uint64_t)max_stream_blocks();
+  const uint64_t cap = (uint64_t)max_stream_blocks() / 8 * (uint64_t)bpc;
   if (b > cap) b = cap;
   const unsigned g = b ? (unsigned)b : 1u;
   switch (mode) {

@@ -103,7 +103,7 @@ for st in "$@"; do
     strided)
           # the strided run's kernels alone (tools/pmc_targets.py): kernel stats
           # and PMC traffic of a 4- and an 8-request run, Push and Pull
-          for t in strided4push strided4pull strided8push strided8pull; do
+          for t in ${STRIDED_TARGETS:-strided4push strided4pull strided8push strided8pull}; do
             rm -rf gpurun_out/prof_$t
             step 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$t -o run --output-format csv -- python3 tools/pmc_targets.py $t 20 > gpurun_out/prof_$t.log 2>&1; echo "$t rc=$?"
             python3 - "$t" <<'PY'
