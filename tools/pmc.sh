@@ -19,7 +19,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 mkdir -p "$R/$out"
 cmd=("$@")
 case "${cmd[0]}" in /*) ;; *) [ -e "$R/${cmd[0]}" ] && cmd[0]="$R/${cmd[0]}" ;; esac
-cd /tmp && export TMPDIR=/tmp
+cd "$R" && export TMPDIR=/tmp  # (from the repo root: relative paths in COMMAND stay valid)
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf "$R/$out/$name.$c"
   env "${envs[@]}" timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$R/$out/$name.$c" -- "${cmd[@]}" > "$R/$out/$name.$c.log" 2>&1
