@@ -1332,6 +1332,20 @@ def run_dropin(args, n_gpus: int) -> dict:
     roof["alg_bytes_note"] = (f"per GPU per step: {N} Push + {N} Pull requests of {n // N} keys per server "
                               f"x {KEYED_PUSH_BYTES} / {KEYED_PULL_BYTES} B per key, {N // gpus if gpus else N} "
                               "server(s) per GPU")
+    # HBM traffic per step of this very job (every kernel of every node), from
+    # the committed PMC passes at two step counts (tools/gpu_run.sh pmcdropin,
+    # tools/pmc_total.py), when one was taken at this N, mode and layout
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_dropin_n{N}_{args.dropin_mode}_l"
+                                                         f"{args.dropin_layout}.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("alg_bytes_per_step") == per_gpu and gpus == 1:
+            roof["traffic"] = d["hbm_bytes_per_step"]
+            roof["traffic_source"] = os.path.relpath(f, ROOT)
+            break
     res = {
         "metric": "device-resident KV Push+Pull GB/s (float vals) through KVWorker/KVServer",
         "value": round(gbs, 3), "unit": "GB/s", "n_gpus": gpus, "steps": args.steps, "warmup": args.warmup,
@@ -1381,7 +1395,9 @@ def roofline(alg_bytes: int, ms: float, args, kernel: str, vb: int, store_extra:
     traffic, source = None, None
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
-    files += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")))
+    # (the newest round's summaries first: a later kernel may be described by
+    # a text that also names an older one)
+    files += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")), reverse=True)
     for pmc in files:
         try:
             d = json.load(open(pmc))

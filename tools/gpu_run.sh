@@ -21,6 +21,7 @@
 #   strided  kernel stats of strided runs alone (4 / 8 requests, Push / Pull)
 #   pmcstrided  PMC traffic of the 4-request strided Push and Pull passes
 #   pmccalib the gfx950 PMC calibration passes (tools/_bin/probe_pmc_shapes)
+#   pmcdropin:N:MODE  HBM traffic per step of the drop-in line (two step counts, differenced)
 #   pmcpull / pmcadam  PMC traffic of the 256 M Pull / the 64 M-feature Adam apply
 #            (tools/pmc_targets.py, two passes each)
 set -u
@@ -120,7 +121,9 @@ PY
           done ;;
     pmcstrided)
           bash tools/pmc.sh gpurun_out/pmc_strided s4push 'k_run_pass<0, 0>|k_run_pass<0, 1>' 10000000 28 python3 tools/pmc_targets.py strided4push 10 && cat gpurun_out/pmc_strided/s4push.json
-          bash tools/pmc.sh gpurun_out/pmc_strided s4pull 'k_run_pass<0, 2>' 10000000 24 python3 tools/pmc_targets.py strided4pull 10 && cat gpurun_out/pmc_strided/s4pull.json ;;
+          bash tools/pmc.sh gpurun_out/pmc_strided s4pull 'k_run_pass<0, 2>' 10000000 24 python3 tools/pmc_targets.py strided4pull 10 && cat gpurun_out/pmc_strided/s4pull.json
+          bash tools/pmc.sh gpurun_out/pmc_strided s8push 'k_run_pass<0, 0>|k_run_pass<0, 1>' 10000000 28 python3 tools/pmc_targets.py strided8push 10 && cat gpurun_out/pmc_strided/s8push.json
+          bash tools/pmc.sh gpurun_out/pmc_strided s8pull 'k_run_pass<0, 2>' 10000000 24 python3 tools/pmc_targets.py strided8pull 10 && cat gpurun_out/pmc_strided/s8pull.json ;;
     pmccalib)
           # the gfx950 FETCH/WRITE calibration per access shape:
           # four counter passes and a trace over tools/_bin/probe_pmc_shapes
@@ -140,6 +143,21 @@ PY
           md=""; [ "$dm" = procs ] && md="-procs"
           PS_RUN_GATHER_US=${dg:-0} PS_STAGE_TIMES=1 step 200 tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dstage_$tag.log 2>&1; echo "$st rc=$?"; grep '"rank": 0' gpurun_out/dstage_$tag.log | cut -c1-300
           python3 tools/stage_summary.py gpurun_out/dstage_$tag.log 40 ;;
+    pmcdropin:*)
+          # pmcdropin:N:mode — HBM traffic per step of the drop-in line (layout 0,
+          # the default gather window): FETCH / WRITE passes of kv_bench_dropin at
+          # 10 and 40 timed steps, differenced (tools/pmc_total.py)
+          # (PMC_GATHER_US: the servers' gather window for these passes — under
+          # counter collection every dispatch is serialized, so the requests of a
+          # step reach a server spread out and, with the default window, fewer
+          # runs form than in the unprofiled line)
+          IFS=: read -r _ dn dm <<< "$st"; tag="n${dn}_${dm}"; o=gpurun_out/pmc_dropin_$tag; rm -rf "$o"; mkdir -p "$o"
+          export PS_RUN_GATHER_US=${PMC_GATHER_US:-120}
+          md=""; [ "$dm" = procs ] && md="-procs"
+          for sN in 10 40; do for c in FETCH_SIZE WRITE_SIZE; do
+            step 240 rocprofv3 --pmc $c --output-format csv -d "$o/$c.$sN" -- tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 $sN 5 0 > "$o/$c.$sN.log" 2>&1 || { echo "pmcdropin pass $c $sN failed"; exit 1; }
+          done; done
+          python3 tools/pmc_total.py "$o/FETCH_SIZE.10" "$o/WRITE_SIZE.10" "$o/FETCH_SIZE.40" "$o/WRITE_SIZE.40" 10 40 $((52 * 10000000 * dn)) "$o/traffic.json" "kv_bench_dropin -ns $dn -nw $dn $md, 10 M keys per worker, layout 0, gather window $PS_RUN_GATHER_US us; alg bytes per step: (28 + 24) B x 10 M keys x $dn workers"; unset PS_RUN_GATHER_US ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
