@@ -297,11 +297,11 @@ int pass_t(int mode, void* store_vals, const uint64_t* K, uint64_t S, const RunF
            const RunDesc* desc, const RunDesc& given, int* bad, int seq, int* flag, hipStream_t st) {
   using T = typename Elem<DT>::T;
   // one lane per 16-B chunk, grid-strided past the cap: PSG_RUN_BPC blocks of
-  // 256 per CU (default 8, the streaming grid)
+  // 256 per CU (default 8, the streaming grid; up to 256, i.e. no cap)
   static const int bpc = [] {
     const char* e = getenv("PSG_RUN_BPC");
     const int v = e ? atoi(e) : 0;
-    return v >= 1 && v <= 32 ? v : 8;
+    return v >= 1 && v <= 256 ? v : 8;
   }();
   uint64_t b = (max_rows + kBlock - 1) / kBlock;
   const uint64_t cap = (uint64_t)max_stream_blocks() / 8 * (uint64_t)bpc;

@@ -170,6 +170,17 @@ inline int RunGatherMicros() {
   }();
   return us;
 }
+/* PS_RUN_GATHER_AUTO=<cap µs> (default 0: off): the gather window follows how
+ * long this server's recent runs took (at least PS_RUN_GATHER_US, at most the
+ * cap) — a sender missing from a run is most likely waiting for another
+ * server's run of about that length before it sends its next request. */
+inline int RunGatherAutoCap() {
+  static const int us = [] {
+    const char* e = std::getenv("PS_RUN_GATHER_AUTO");
+    return e ? std::atoi(e) : 0;
+  }();
+  return us;
+}
 /* PS_TRACE_REQUESTS=<file>: every request a KVServer hands to its handle is
  * appended to <file> as one line "server sender timestamp push pull keys
  * run_size run_pos" (run_size 1 for a request handled on its own) — the
@@ -468,6 +479,7 @@ class KVServer : public SimpleApp {
   unsigned recent_n_ = 0;
   int gather_idle_ = 0;  // gather windows in a row that timed out with nothing gained
   int gather_cool_ = 0;  // requests left to take without a window
+  double run_us_ = 0;    // this server's recent run times (moving average, µs)
   void NoteSender(int sender) { recent_[recent_n_++ & 63] = sender; }
   size_t RecentSenders(int sender) {
     NoteSender(sender);
@@ -919,7 +931,9 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     // the queue is a message that may not join.
     // A window that keeps timing out with nothing gained (a sender stopped
     // sending) is skipped for the next 64 requests.
-    const int gather_us = gather_cool_ > 0 ? 0 : detail::RunGatherMicros();
+    int gather_us = gather_cool_ > 0 ? 0 : detail::RunGatherMicros();
+    if (gather_us > 0 && detail::RunGatherAutoCap() > 0)
+      gather_us = std::min(detail::RunGatherAutoCap(), std::max(gather_us, (int)run_us_));
     if (gather_cool_ > 0) --gather_cool_;
     const size_t want = gather_us > 0 ? RecentSenders(meta.sender) : 0;
     const auto t_gather = std::chrono::steady_clock::now();
@@ -959,7 +973,10 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       direct_out_ = SVector<Value>();
       for (size_t j = 0; j < items.size(); ++j)
         detail::TraceRequest(PostOffice::Get()->my_id(), items[j].meta, items[j].data.keys.size(), items.size(), j);
+      const auto t_run = std::chrono::steady_clock::now();
       run(items, this);
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_run).count();
+      run_us_ = run_us_ > 0 ? 0.75 * run_us_ + 0.25 * us : us;
       return;
     }
   }
