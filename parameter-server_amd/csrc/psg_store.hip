@@ -769,6 +769,9 @@ __global__ __launch_bounds__(1024, 8) void k_validate_code(const uint64_t* __res
 // rej[kRejList]: the lean apply then writes nothing and the host validates
 // the request in full (W_NOTLIST).  One lane per 4 keys, grid-strided; the
 // tile words by the lanes of each tile's first keys.
+constexpr int kIdU = 2;  // groups of 4 keys in flight per lane (k_list_check, k_ident_check)
+
+template <int NT>
 __global__ __launch_bounds__(256) void k_list_check(const uint64_t* __restrict__ q,
                                                     const uint64_t* __restrict__ copy, uint64_t n,
                                                     const Win* __restrict__ win, uint32_t gen,
@@ -776,30 +779,47 @@ __global__ __launch_bounds__(256) void k_list_check(const uint64_t* __restrict__
                                                     uint32_t* __restrict__ tword) {
   constexpr uint64_t tileN = 1024 * kPerLane;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   int bad = 0;
-  const uint64_t nq = (n + 3) / 4;
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < nq; j += stride) {
-    const uint64_t i0 = 4 * j;
-    if (i0 + 4 <= n && vec) {
-      const u64x2 a0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0));
-      const u64x2 a1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(q + i0) + 1);
-      const u64x2 b0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(copy + i0));
-      const u64x2 b1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(copy + i0) + 1);
-      if (a0[0] != b0[0] || a0[1] != b0[1] || a1[0] != b1[0] || a1[1] != b1[1]) bad = 1;
-    } else {
-      for (uint64_t i = i0; i < n && i < i0 + 4; ++i)
-        if (q[i] != copy[i]) bad = 1;
-    }
-    if ((i0 % tileN) == 0) {
-      const uint64_t tile = i0 / tileN;
-      const uint64_t t1 = (i0 + tileN < n) ? i0 + tileN : n;
-      const Win e = win[tile];
-      const bool cur = e.gen == gen && e.lo <= e.hi;
-      const uint64_t W = cur ? (uint64_t)(e.hi - e.lo) : 0;
-      if (!cur || W < t1 - i0 || W > 2 * tileN) bad = 1;
-      tword[tile] = tile_tag(seq) | (W == t1 - i0 ? kTileStretch : kTileCoded);
+  // the tile words: one lane per tile
+  const uint64_t ntiles = (n + tileN - 1) / tileN;
+  for (uint64_t tile = gid; tile < ntiles; tile += stride) {
+    const uint64_t i0 = tile * tileN;
+    const uint64_t t1 = (i0 + tileN < n) ? i0 + tileN : n;
+    const Win e = win[tile];
+    const bool cur = e.gen == gen && e.lo <= e.hi;
+    const uint64_t W = cur ? (uint64_t)(e.hi - e.lo) : 0;
+    if (!cur || W < t1 - i0 || W > 2 * tileN) bad = 1;
+    tword[tile] = tile_tag(seq) | (W == t1 - i0 ? kTileStretch : kTileCoded);
+  }
+  // the compare: groups of 4 keys (two 16-B loads of each array), kIdU groups
+  // per lane in flight (k_ident_check's shape)
+  uint64_t done = 0;
+  if (vec) {
+    const uint64_t ng = n / 4;
+    done = ng * 4;
+    for (uint64_t b = (uint64_t)blockIdx.x * kBlock * kIdU + threadIdx.x; b < ng; b += stride * kIdU) {
+      u64x2 a[kIdU][2], c[kIdU][2];
+#pragma unroll
+      for (int u = 0; u < kIdU; ++u) {
+        const uint64_t j = b + (uint64_t)u * kBlock < ng ? b + (uint64_t)u * kBlock : b;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u64x2* pq = reinterpret_cast<const u64x2*>(q + 4 * j + 2 * h);
+          const u64x2* pc = reinterpret_cast<const u64x2*>(copy + 4 * j + 2 * h);
+          a[u][h] = NT ? __builtin_nontemporal_load(pq) : *pq;
+          c[u][h] = NT ? __builtin_nontemporal_load(pc) : *pc;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kIdU; ++u)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (a[u][h][0] != c[u][h][0] || a[u][h][1] != c[u][h][1]) bad = 1;
     }
   }
+  for (uint64_t i = done + gid; i < n; i += stride)
+    if (q[i] != copy[i]) bad = 1;
   if (__ballot(bad) && (threadIdx.x & 63) == 0) rej[kRejList] = seq;
 }
 
@@ -1626,7 +1646,6 @@ __global__ __launch_bounds__(NT, (WM == 2 ? 8 : 4)) void k_resolve_apply(const u
 // W_NOTIDENT, raising kPending like any follow-up, and the host serves it again
 // on the general path.
 
-constexpr int kIdU = 2;  // groups of 4 keys in flight per lane
 
 // The stretch's first slot, uniform: tile 0's cached window is current and is
 // for this first key, and n slots fit from it.
@@ -2709,9 +2728,25 @@ static int launch_fused(psg_store* s, int op, const uint64_t* q, uint64_t n, con
   const bool use_vl = vl_ok && wc->copy && wc->copy_cap >= n && wc->copy_gen == s->gen;
   const bool learn = vl_ok && wc->copy && wc->copy_cap >= n && !use_vl;
   if (use_vl) {
-    const unsigned gl = grid_n((n + 3) / 4, kBlock);
-    k_list_check<<<gl, kBlock, 0, st>>>(q, wc->copy, n, win, s->gen, s->reject_dev, seq,
-                                        aligned16(q) && aligned16(wc->copy) ? 1 : 0, tile_words(s, s->ring_next));
+    // PSG_LC_BPC (A/B): blocks per CU (default 8); PSG_LC_NT=1: non-temporal loads
+    static const int lc_bpc = [] {
+      const char* e = getenv("PSG_LC_BPC");
+      const int v = e ? atoi(e) : 0;
+      return v >= 1 && v <= 32 ? v : 8;
+    }();
+    static const bool lc_nt = [] {
+      const char* e = getenv("PSG_LC_NT");
+      return e && atoi(e) != 0;
+    }();
+    const unsigned gl = std::min<unsigned>(grid_n(n, (uint64_t)kBlock * 4 * kIdU),
+                                           (unsigned)(max_stream_blocks() / 8) * (unsigned)lc_bpc);
+    const int lvec = aligned16(q) && aligned16(wc->copy) ? 1 : 0;
+    if (lc_nt)
+      k_list_check<1><<<gl, kBlock, 0, st>>>(q, wc->copy, n, win, s->gen, s->reject_dev, seq, lvec,
+                                             tile_words(s, s->ring_next));
+    else
+      k_list_check<0><<<gl, kBlock, 0, st>>>(q, wc->copy, n, win, s->gen, s->reject_dev, seq, lvec,
+                                             tile_words(s, s->ring_next));
     s->counters[PSG_CTR_LISTS]++;
   } else if (coded_ran) {
     const unsigned cus = (unsigned)(max_stream_blocks() / 8);
