@@ -126,7 +126,7 @@ __global__ __launch_bounds__(1024) void k_run_classify(const uint64_t* __restric
   }
 }
 
-template <int DT, int MODE>
+template <int DT, int MODE, int U, int NT>
 __global__ __launch_bounds__(256) void k_run_pass(typename Elem<DT>::T* __restrict__ store,
                                                   const uint64_t* __restrict__ K, uint64_t S, RunFrames f,
                                                   const RunDesc* __restrict__ dp, RunDesc given,
@@ -184,102 +184,116 @@ __global__ __launch_bounds__(256) void k_run_pass(typename Elem<DT>::T* __restri
   __syncthreads();
   const uint64_t D = sD, rows = srows;
   const uint32_t P = sP;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   // One lane per 16-B chunk of store values (V slots) over the rows' slots
   // [D, D + P rows): every wave instruction on the store's keys and values is
   // one contiguous run, whatever P.  A chunk's slots are consecutive phases,
-  // wrapping into the next row: one division per chunk.
+  // wrapping into the next row: one division per chunk.  U chunks per lane at
+  // a time (kBlock apart, so each wave instruction stays one contiguous run):
+  // every load of the U chunks is issued before the first one is used.
   const uint64_t end = D + (uint64_t)P * rows;
   const uint64_t c0 = D / V, c1 = (end + V - 1) / V;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock * U;
   int mismatch = 0;
-  for (uint64_t t = c0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < c1; t += stride) {
-    const uint64_t a0 = t * V;
-    int ph[V], ops[V];
-    uint32_t rw[V];
-    {
+  for (uint64_t t0 = c0 + (uint64_t)blockIdx.x * kBlock * U + threadIdx.x; t0 < c1; t0 += stride) {
+    int ph[U][V], ops[U][V];
+    uint32_t rw[U][V];
+    bool whole[U], anypush[U];
+    uint64_t a0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t t = t0 + (uint64_t)u * kBlock;
+      a0[u] = t * V;
       // the phase and row of the chunk's first slot (slots before D: none)
-      const uint64_t m0 = a0 >= D ? a0 - D : 0;
+      const uint64_t m0 = a0[u] >= D ? a0[u] - D : 0;
       uint32_t r = (uint32_t)(m0 / P);
       uint32_t p = (uint32_t)(m0 - (uint64_t)r * P);
+      anypush[u] = false;
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const uint64_t a = a0 + e;
-        const bool in = a >= D && a < end;
-        ph[e] = in ? (int)p : 0;
-        rw[e] = r;
-        ops[e] = in && r < sn[p] ? sop[p] : 0;
+        const uint64_t a = a0[u] + e;
+        const bool in = t < c1 && a >= D && a < end;
+        ph[u][e] = in ? (int)p : 0;
+        rw[u][e] = r;
+        ops[u][e] = in && r < sn[p] ? sop[p] : 0;
+        anypush[u] = anypush[u] || (ops[u][e] & PSG_PUSH);
         if (a >= D && ++p == P) {
           p = 0;
           ++r;
         }
       }
+      whole[u] = a0[u] + V <= S;
     }
-    bool anyop = false, anypush = false;
+    // every load of the U chunks first, then the arithmetic, then the writes
+    uint64_t kk[U][V], qq[U][V];
+    T y[U][V], av[U][V];
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      anyop = anyop || ops[e];
-      anypush = anypush || (ops[e] & PSG_PUSH);
-    }
-    if (!anyop) continue;
-    const bool whole = a0 + V <= S;
-    // every load of the chunk first, then the arithmetic, then the writes
-    uint64_t kk[V], qq[V];
-    if constexpr (MODE != RUN_APPLY) {
-      if (whole) {
-        const u64x2* kp = reinterpret_cast<const u64x2*>(K + a0);
+    for (int u = 0; u < U; ++u) {
+      bool anyop = false;
 #pragma unroll
-        for (int h = 0; h < V / 2; ++h) {
-          const u64x2 x = __builtin_nontemporal_load(kp + h);
-          kk[2 * h] = x[0];
-          kk[2 * h + 1] = x[1];
-        }
-      } else {
+      for (int e = 0; e < V; ++e) anyop = anyop || ops[u][e];
+      if constexpr (MODE != RUN_APPLY) {
+        if (anyop && whole[u]) {
+          const u64x2* kp = reinterpret_cast<const u64x2*>(K + a0[u]);
 #pragma unroll
-        for (int e = 0; e < V; ++e) kk[e] = ops[e] ? K[a0 + e] : 0;
-      }
-#pragma unroll
-      for (int e = 0; e < V; ++e) qq[e] = ops[e] ? __builtin_nontemporal_load(sq[ph[e]] + rw[e]) : 0;
-    }
-    T x[V];
-    if constexpr (MODE != RUN_CHECK) {
-      T y[V];
-      if (whole) {
-        typedef T tv __attribute__((ext_vector_type(V)));
-        const tv w = __builtin_bit_cast(tv, *reinterpret_cast<const u32x4*>(store + a0));
-#pragma unroll
-        for (int e = 0; e < V; ++e) y[e] = w[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < V; ++e) y[e] = ops[e] ? store[a0 + e] : T(0);
-      }
-      T a[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) a[e] = (ops[e] & PSG_PUSH) ? __builtin_nontemporal_load(sv[ph[e]] + rw[e]) : T(0);
-#pragma unroll
-      for (int e = 0; e < V; ++e) x[e] = (ops[e] & PSG_PUSH) ? E::add1(y[e], a[e]) : y[e];
-    }
-    if constexpr (MODE != RUN_APPLY) {
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        if (ops[e] && qq[e] != kk[e]) mismatch = 1;
-    }
-    if constexpr (MODE != RUN_CHECK) {
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        if (ops[e] & PSG_PULL) __builtin_nontemporal_store(x[e], so[ph[e]] + rw[e]);
-      if (MODE == RUN_APPLY && anypush) {
-        if (whole) {
-          typedef T tv __attribute__((ext_vector_type(V)));
-          tv w;
-#pragma unroll
-          for (int e = 0; e < V; ++e) w[e] = x[e];
-          // the chunk's slots no request of the run holds go back unchanged:
-          // only this stream writes the store
-          *reinterpret_cast<u32x4*>(store + a0) = __builtin_bit_cast(u32x4, w);
+          for (int h = 0; h < V / 2; ++h) {
+            const u64x2 x = NT ? __builtin_nontemporal_load(kp + h) : kp[h];
+            kk[u][2 * h] = x[0];
+            kk[u][2 * h + 1] = x[1];
+          }
         } else {
 #pragma unroll
-          for (int e = 0; e < V; ++e)
-            if (ops[e] & PSG_PUSH) store[a0 + e] = x[e];
+          for (int e = 0; e < V; ++e) kk[u][e] = ops[u][e] ? K[a0[u] + e] : 0;
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          qq[u][e] = ops[u][e] ? (NT ? __builtin_nontemporal_load(sq[ph[u][e]] + rw[u][e]) : sq[ph[u][e]][rw[u][e]])
+                               : 0;
+      }
+      if constexpr (MODE != RUN_CHECK) {
+        if (anyop && whole[u]) {
+          typedef T tv __attribute__((ext_vector_type(V)));
+          const tv w = __builtin_bit_cast(tv, *reinterpret_cast<const u32x4*>(store + a0[u]));
+#pragma unroll
+          for (int e = 0; e < V; ++e) y[u][e] = w[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) y[u][e] = ops[u][e] ? store[a0[u] + e] : T(0);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          av[u][e] = (ops[u][e] & PSG_PUSH)
+                         ? (NT ? __builtin_nontemporal_load(sv[ph[u][e]] + rw[u][e]) : sv[ph[u][e]][rw[u][e]])
+                         : T(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (MODE != RUN_APPLY) {
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (ops[u][e] && qq[u][e] != kk[u][e]) mismatch = 1;
+      }
+      if constexpr (MODE != RUN_CHECK) {
+        T x[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) x[e] = (ops[u][e] & PSG_PUSH) ? E::add1(y[u][e], av[u][e]) : y[u][e];
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (ops[u][e] & PSG_PULL) __builtin_nontemporal_store(x[e], so[ph[u][e]] + rw[u][e]);
+        if (MODE == RUN_APPLY && anypush[u]) {
+          if (whole[u]) {
+            typedef T tv __attribute__((ext_vector_type(V)));
+            tv w;
+#pragma unroll
+            for (int e = 0; e < V; ++e) w[e] = x[e];
+            // the chunk's slots no request of the run holds go back unchanged:
+            // only this stream writes the store
+            *reinterpret_cast<u32x4*>(store + a0[u]) = __builtin_bit_cast(u32x4, w);
+          } else {
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              if (ops[u][e] & PSG_PUSH) store[a0[u] + e] = x[e];
+          }
         }
       }
     }
@@ -303,21 +317,39 @@ int pass_t(int mode, void* store_vals, const uint64_t* K, uint64_t S, const RunF
     const int v = e ? atoi(e) : 0;
     return v >= 1 && v <= 256 ? v : 8;
   }();
-  uint64_t b = (max_rows + kBlock - 1) / kBlock;
+  // PSG_RUN_U (A/B): chunks per lane in flight (1 or 2; default 1 — two
+  // measured slower, profiles/r6_strided_units_ab.txt); PSG_RUN_NT=0 (A/B):
+  // the request arrays and store keys read as plain loads — faster for a run
+  // alone (check 0.65 -> 0.72, apply 0.65 -> 0.69, Pull 0.70 -> 0.74 at P = 4)
+  // but slower in the drop-in job, where N servers' passes share the chip
+  // (0.642 vs 0.585 ms a step at N = 4, profiles/r6_strided_units_ab.txt)
+  static const int units = [] {
+    const char* e = getenv("PSG_RUN_U");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  static const int nt = [] {
+    const char* e = getenv("PSG_RUN_NT");
+    return e && atoi(e) == 0 ? 0 : 1;
+  }();
+  uint64_t b = (max_rows + (uint64_t)kBlock * units - 1) / ((uint64_t)kBlock * units);
   const uint64_t cap = (uint64_t)max_stream_blocks() / 8 * (uint64_t)bpc;
   if (b > cap) b = cap;
   const unsigned g = b ? (unsigned)b : 1u;
+#define PSG_RUN_LAUNCH(M, UU, N) \
+  k_run_pass<DT, M, UU, N><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag)
+#define PSG_RUN_BY_U(M)                                   \
+  do {                                                    \
+    if (units == 2) PSG_RUN_LAUNCH(M, 2, 1);              \
+    else if (nt) PSG_RUN_LAUNCH(M, 1, 1);                 \
+    else PSG_RUN_LAUNCH(M, 1, 0);                         \
+  } while (0)
   switch (mode) {
-    case RUN_CHECK:
-      k_run_pass<DT, RUN_CHECK><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag);
-      break;
-    case RUN_APPLY:
-      k_run_pass<DT, RUN_APPLY><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag);
-      break;
-    default:
-      k_run_pass<DT, RUN_PULL_CHECKED><<<g, kBlock, 0, st>>>((T*)store_vals, K, S, f, desc, given, bad, seq, flag);
-      break;
+    case RUN_CHECK: PSG_RUN_BY_U(RUN_CHECK); break;
+    case RUN_APPLY: PSG_RUN_BY_U(RUN_APPLY); break;
+    default: PSG_RUN_BY_U(RUN_PULL_CHECKED); break;
   }
+#undef PSG_RUN_BY_U
+#undef PSG_RUN_LAUNCH
   PSG_HIP(hipGetLastError());
   return PSG_OK;
 }

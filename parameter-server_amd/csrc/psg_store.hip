@@ -874,7 +874,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_apply(uint64_t n, const Win* _
     const bool whole = i0 + kPerLane <= t1;
     T v[kPerLane];
     if (whole && (vec & 1)) {
-      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + i0)));
+      const f32x4 x = __builtin_bit_cast(f32x4, ((vec & 16) ? *reinterpret_cast<const u32x4*>(vals + i0) : __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + i0))));
 #pragma unroll
       for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
     } else {
@@ -1023,7 +1023,7 @@ __device__ __forceinline__ void tile_apply_step(uint64_t tile, uint64_t n, uint6
   const bool whole = i0 + kPerLane <= t1;
   T v[kPerLane];
   if (whole && (vec & 1)) {
-    const f32x4 x = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + i0)));
+    const f32x4 x = __builtin_bit_cast(f32x4, ((vec & 16) ? *reinterpret_cast<const u32x4*>(vals + i0) : __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + i0))));
 #pragma unroll
     for (int k = 0; k < kPerLane; ++k) v[k] = x[k];
   } else {
@@ -1754,7 +1754,8 @@ __global__ __launch_bounds__(256) void k_ident_apply(const uint64_t* __restrict_
             x[u] = __builtin_bit_cast(f32x4, (vec & 8) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Vd + 4 * j[u]))
                                                        : *reinterpret_cast<const u32x4*>(Vd + 4 * j[u]));
             if constexpr (PUSH) {
-              v[u] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals) + j[u]));
+              v[u] = __builtin_bit_cast(f32x4, (vec & 16) ? reinterpret_cast<const u32x4*>(vals)[j[u]]
+                                                        : __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals) + j[u]));
             } else {
 #pragma unroll
               for (int h = 0; h < 2; ++h) {
@@ -2550,7 +2551,13 @@ static void launch_tile_apply(psg_store* s, uint64_t n, const void* vals, void* 
       return e ? atoi(e) : 2;
     }();
     const unsigned g = (unsigned)(ta_bpc > 0 ? std::min<uint64_t>(ntiles, (uint64_t)cus * ta_bpc) : ntiles);
-    const int vec = ((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0;
+    // PSG_TA_NT=0 (A/B): the request's values read as plain loads (vec bit 4)
+    static const int ta_nt = [] {
+      const char* e = getenv("PSG_TA_NT");
+      return e ? atoi(e) : 1;
+    }();
+    const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
+                    (ta_nt ? 0 : 16);
     Arrival arr;
     arr.ctr = s->done_ctr + (uint64_t)rec.ring * (kArriveShards + 1) * kArriveStride;
     static const bool db = [] {
@@ -2599,13 +2606,15 @@ static void launch_ident(psg_store* s, const uint64_t* q, uint64_t n, const void
   const unsigned cus = (unsigned)(max_stream_blocks() / 8);
   const unsigned g = std::min<unsigned>(g0, cus * (unsigned)id_bpc);
   const unsigned gc = std::min<unsigned>(g0, cus * (unsigned)idc_bpc);
-  // PSG_ID_NT (A/B): bit 0 the store values written non-temporally, bit 1 read so
+  // PSG_ID_NT (A/B): bit 0 the store values written non-temporally, bit 1 read so,
+  // bit 2 the request's values read as plain loads
   static const int id_nt = [] {
     const char* e = getenv("PSG_ID_NT");
     return e ? atoi(e) : 0;
   }();
   const int vec = (((OP & PSG_PUSH) == 0 || aligned16(vals)) && ((OP & PSG_PULL) == 0 || aligned16(out)) ? 1 : 0) |
-                  (aligned16(q) ? 2 : 0) | ((id_nt & 1) ? 4 : 0) | ((id_nt & 2) ? 8 : 0);
+                  (aligned16(q) ? 2 : 0) | ((id_nt & 1) ? 4 : 0) | ((id_nt & 2) ? 8 : 0) |
+                  ((id_nt & 4) ? 16 : 0);
   if (OP & PSG_PUSH)
     k_ident_check<<<gc, kBlock, 0, st>>>(q, n, s->keys, s->size, win, s->gen, s->reject_dev, s->seq, vec);
   Arrival arr;

@@ -114,16 +114,16 @@ for r in csv.DictReader(open(f"gpurun_out/prof_{t}/run_kernel_stats.csv")):
     n = r["Name"]
     if "k_run" in n:
         avg = float(r["AverageNs"]) / 1e3
-        per = 16 if "k_run_pass<0, 0>" in n else (12 if "k_run_pass<0, 1>" in n else (24 if "k_run_pass<0, 2>" in n else 0))
+        per = 16 if "k_run_pass<0, 0" in n else (12 if "k_run_pass<0, 1" in n else (24 if "k_run_pass<0, 2" in n else 0))
         frac = (per * 10e6 / (avg * 1e-6) / 8e12) if per else 0
         print(f"  {n[:60]:60s} calls {r['Calls']:>4} avg {avg:8.1f} us  {per} B/key -> {frac:.3f} of 8 TB/s")
 PY
           done ;;
     pmcstrided)
-          bash tools/pmc.sh gpurun_out/pmc_strided s4push 'k_run_pass<0, 0>|k_run_pass<0, 1>' 10000000 28 python3 tools/pmc_targets.py strided4push 10 && cat gpurun_out/pmc_strided/s4push.json
-          bash tools/pmc.sh gpurun_out/pmc_strided s4pull 'k_run_pass<0, 2>' 10000000 24 python3 tools/pmc_targets.py strided4pull 10 && cat gpurun_out/pmc_strided/s4pull.json
-          bash tools/pmc.sh gpurun_out/pmc_strided s8push 'k_run_pass<0, 0>|k_run_pass<0, 1>' 10000000 28 python3 tools/pmc_targets.py strided8push 10 && cat gpurun_out/pmc_strided/s8push.json
-          bash tools/pmc.sh gpurun_out/pmc_strided s8pull 'k_run_pass<0, 2>' 10000000 24 python3 tools/pmc_targets.py strided8pull 10 && cat gpurun_out/pmc_strided/s8pull.json ;;
+          bash tools/pmc.sh gpurun_out/pmc_strided s4push 'k_run_pass<0, 0|k_run_pass<0, 1' 10000000 28 python3 tools/pmc_targets.py strided4push 10 && cat gpurun_out/pmc_strided/s4push.json
+          bash tools/pmc.sh gpurun_out/pmc_strided s4pull 'k_run_pass<0, 2' 10000000 24 python3 tools/pmc_targets.py strided4pull 10 && cat gpurun_out/pmc_strided/s4pull.json
+          bash tools/pmc.sh gpurun_out/pmc_strided s8push 'k_run_pass<0, 0|k_run_pass<0, 1' 10000000 28 python3 tools/pmc_targets.py strided8push 10 && cat gpurun_out/pmc_strided/s8push.json
+          bash tools/pmc.sh gpurun_out/pmc_strided s8pull 'k_run_pass<0, 2' 10000000 24 python3 tools/pmc_targets.py strided8pull 10 && cat gpurun_out/pmc_strided/s8pull.json ;;
     pmccalib)
           # the gfx950 FETCH/WRITE calibration per access shape:
           # four counter passes and a trace over tools/_bin/probe_pmc_shapes
