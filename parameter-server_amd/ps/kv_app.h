@@ -181,6 +181,28 @@ inline int RunGatherAutoCap() {
   }();
   return us;
 }
+/* PS_RUN_GATHER_ORDINAL (default 1): the gather waits only for the recent
+ * senders that are behind the run — those this server has taken fewer
+ * requests from than the run's lowest ordinal (its n-th request from each) —
+ * and for up to PS_RUN_GATHER_ORD_US (default 1000) µs.  A sender that is not
+ * behind has had this round's request served already and may itself wait for
+ * this server's answer to another; one that is behind is held up only by
+ * servers serving lower ordinals, so the waits form no cycle.  0: wait for
+ * every recent sender for PS_RUN_GATHER_US (A/B). */
+inline bool RunGatherOrdinal() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_RUN_GATHER_ORDINAL");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+inline int RunGatherOrdMicros() {
+  static const int us = [] {
+    const char* e = std::getenv("PS_RUN_GATHER_ORD_US");
+    return e ? std::atoi(e) : 1000;
+  }();
+  return us;
+}
 /* PS_TRACE_REQUESTS=<file>: every request a KVServer hands to its handle is
  * appended to <file> as one line "server sender timestamp push pull keys
  * run_size run_pos" (run_size 1 for a request handled on its own) — the
@@ -480,6 +502,24 @@ class KVServer : public SimpleApp {
   int gather_idle_ = 0;  // gather windows in a row that timed out with nothing gained
   int gather_cool_ = 0;  // requests left to take without a window
   double run_us_ = 0;    // this server's recent run times (moving average, µs)
+  // requests taken from each sender so far (a request's ordinal: the n-th from
+  // its sender)
+  std::unordered_map<int, uint64_t> taken_;
+  uint64_t Take(int sender) { return ++taken_[sender]; }
+  // a recent sender outside the run that this server has taken fewer than m
+  // requests from (its next request is the run's round or an earlier one)
+  bool SendersBehind(const std::vector<KVRunItem<Value>>& items, uint64_t m) {
+    const unsigned n = recent_n_ < 64 ? recent_n_ : 64;
+    for (unsigned i = 0; i < n; ++i) {
+      const int w = recent_[i];
+      bool in = false;
+      for (const auto& it : items) in = in || it.meta.sender == w;
+      if (in) continue;
+      auto t = taken_.find(w);
+      if ((t == taken_.end() ? 0 : t->second) < m) return true;
+    }
+    return false;
+  }
   void NoteSender(int sender) { recent_[recent_n_++ & 63] = sender; }
   size_t RecentSenders(int sender) {
     NoteSender(sender);
@@ -848,6 +888,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     return;
   }
   const KVMeta meta = MetaOf(msg);
+  const uint64_t ordinal = Take(meta.sender);
   bool device_frames, installed;
   RunHandle run;
   {
@@ -931,17 +972,22 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     // the queue is a message that may not join.
     // A window that keeps timing out with nothing gained (a sender stopped
     // sending) is skipped for the next 64 requests.
-    int gather_us = gather_cool_ > 0 ? 0 : detail::RunGatherMicros();
-    if (gather_us > 0 && detail::RunGatherAutoCap() > 0)
+    // With the ordinal rule (detail::RunGatherOrdinal) the window waits only
+    // for the senders behind the run, for up to PS_RUN_GATHER_ORD_US.
+    const bool by_ordinal = detail::RunGatherOrdinal() && detail::RunGatherMicros() > 0;
+    int gather_us = gather_cool_ > 0 ? 0 : by_ordinal ? detail::RunGatherOrdMicros() : detail::RunGatherMicros();
+    if (gather_us > 0 && !by_ordinal && detail::RunGatherAutoCap() > 0)
       gather_us = std::min(detail::RunGatherAutoCap(), std::max(gather_us, (int)run_us_));
     if (gather_cool_ > 0) --gather_cool_;
     const size_t want = gather_us > 0 ? RecentSenders(meta.sender) : 0;
+    uint64_t low = ordinal;  // the run's lowest ordinal
     const auto t_gather = std::chrono::steady_clock::now();
     bool waited = false;
     Message next;
     while ((int)items.size() < kMaxRun) {
       if (!customer_->TakeQueued(mate, &next)) {
-        if (items.size() >= want || customer_->Queued() > 0) break;
+        const bool more = gather_us > 0 && (by_ordinal ? SendersBehind(items, low) : items.size() < want);
+        if (!more || customer_->Queued() > 0) break;
         if (std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(gather_us)) {
           if (!waited && ++gather_idle_ >= 4) {
             gather_idle_ = 0;
@@ -957,6 +1003,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
         gather_idle_ = 0;
       }
       NoteSender(next.meta.sender);
+      low = std::min(low, Take(next.meta.sender));
       KVRunItem<Value> it;
       it.meta = MetaOf(next);
       for (const auto& o : items) distinct = distinct && o.meta.sender != it.meta.sender;
