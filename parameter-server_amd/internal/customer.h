@@ -59,10 +59,15 @@ class ThreadsafePQueue {
   /* the message WaitAndPop would return next, popped only when take(it) says
    * so; never waits (a server draining a run of queued Pushes) */
   template <typename Pred>
-  bool PopIf(Pred take, Message* out) {
+  bool PopIf(Pred take, Message* out, bool* refused = nullptr) {
+    if (refused) *refused = false;
     if (size_.load(std::memory_order_acquire) == 0) return false;
     std::lock_guard<std::mutex> lk(mu_);
-    if (queue_.empty() || !take(queue_.top())) return false;
+    if (queue_.empty()) return false;
+    if (!take(queue_.top())) {
+      if (refused) *refused = true;  // the head is there and may not be taken
+      return false;
+    }
     *out = queue_.top();
     queue_.pop();
     size_.store(queue_.size(), std::memory_order_release);
@@ -114,8 +119,8 @@ class Customer {
    * — exactly the one the thread would handle next, so the order of handling
    * is unchanged (a KVServer serving a run of queued Pushes in one pass). */
   template <typename Pred>
-  bool TakeQueued(Pred take, Message* out) {
-    return receive_queue_.PopIf(take, out);
+  bool TakeQueued(Pred take, Message* out, bool* refused = nullptr) {
+    return receive_queue_.PopIf(take, out, refused);
   }
   /* messages waiting in the receive queue (a hint: it may change at once) */
   size_t Queued() const { return receive_queue_.Size(); }

@@ -220,6 +220,22 @@ inline void TraceRequest(int server, const KVMeta& m, size_t keys, size_t run_si
   if (len > 0) (void)!::write(fd, line, (size_t)len);
 }
 
+/* PS_TRACE_GATHER=<file> (diagnostics): one line per gathered run, "server
+ * head_sender head_ordinal run_size why waited_us" — why the gather ended:
+ * 0 run full, 1 no sender behind (or no window), 2 a queued message that
+ * may not join, 3 the window timed out. */
+inline void TraceGather(int server, int sender, uint64_t ordinal, size_t size, int why, double us) {
+  static const int fd = [] {
+    const char* e = std::getenv("PS_TRACE_GATHER");
+    return e && *e ? ::open(e, O_WRONLY | O_CREAT | O_APPEND, 0644) : -1;
+  }();
+  if (fd < 0) return;
+  char line[128];
+  const int len = std::snprintf(line, sizeof(line), "%d %d %llu %zu %d %.1f\n", server, sender,
+                                (unsigned long long)ordinal, size, why, us);
+  if (len > 0) (void)!::write(fd, line, (size_t)len);
+}
+
 /* ZPull offers the servers its HBM output (Meta::direct_reply); PS_DIRECT_REPLY=0
  * turns the offer off (A/B): every reply is then merged by psg_merge. */
 inline bool DirectReplyOn() {
@@ -964,12 +980,13 @@ void KVServer<Value>::OnReceive(const Message& msg) {
         if (it.meta.sender == m.meta.sender) return false;
       return true;
     };
-    // The gather window (PS_RUN_GATHER_US, default 0: off): when fewer
+    // The gather window (PS_RUN_GATHER_US, default 120; 0: off): when fewer
     // requests are queued than the senders this server has heard from lately,
     // wait up to that long for theirs to arrive — the requests of one step
     // reach a server microseconds apart, and a request taken alone costs a
     // whole pass over the store's lines.  The wait ends as soon as the head of
-    // the queue is a message that may not join.
+    // the queue is a message that may not join (PopIf's refusal: a message
+    // that arrives while the window checks its senders is still taken).
     // A window that keeps timing out with nothing gained (a sender stopped
     // sending) is skipped for the next 64 requests.
     // With the ordinal rule (detail::RunGatherOrdinal) the window waits only
@@ -984,15 +1001,26 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     const auto t_gather = std::chrono::steady_clock::now();
     bool waited = false;
     Message next;
+    int why = 0;
     while ((int)items.size() < kMaxRun) {
-      if (!customer_->TakeQueued(mate, &next)) {
+      bool refused = false;
+      if (!customer_->TakeQueued(mate, &next, &refused)) {
+        // (the head of the queue may not join: the run ends here, in queue order)
+        if (refused) {
+          why = 2;
+          break;
+        }
         const bool more = gather_us > 0 && (by_ordinal ? SendersBehind(items, low) : items.size() < want);
-        if (!more || customer_->Queued() > 0) break;
+        if (!more) {
+          why = 1;
+          break;
+        }
         if (std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(gather_us)) {
           if (!waited && ++gather_idle_ >= 4) {
             gather_idle_ = 0;
             gather_cool_ = 64;
           }
+          why = 3;
           break;
         }
         __builtin_ia32_pause();
@@ -1016,6 +1044,8 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     // (a plain request on its own goes to the run handle too: the store
     // serves it as a strided pass when it knows its list's place in a learnt
     // interleaved layout, else as one request)
+    detail::TraceGather(PostOffice::Get()->my_id(), meta.sender, ordinal, items.size(), why,
+                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_gather).count());
     if (items.size() > 1 || detail::MixedRunsOn()) {
       direct_out_ = SVector<Value>();
       for (size_t j = 0; j < items.size(); ++j)

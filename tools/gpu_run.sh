@@ -91,9 +91,9 @@ for st in "$@"; do
     dtrace:*)
           # dtrace:N:mode:layout — kv_bench_dropin with the servers' request trace:
           # run sizes per server (PS_TRACE_REQUESTS) and the store counters
-          IFS=: read -r _ dn dm dl <<< "$st"; tag="n${dn}_${dm}_l${dl}"; rm -f gpurun_out/dtrace_$tag.txt
+          IFS=: read -r _ dn dm dl <<< "$st"; tag="n${dn}_${dm}_l${dl}"; rm -f gpurun_out/dtrace_$tag.txt gpurun_out/dgather_$tag.txt
           md=""; [ "$dm" = procs ] && md="-procs"
-          PS_TRACE_REQUESTS=$PWD/gpurun_out/dtrace_$tag.txt step 200 tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dtrace_$tag.log 2>&1; echo "$st rc=$?"; grep "^{" gpurun_out/dtrace_$tag.log | cut -c1-300
+          PS_TRACE_GATHER=$PWD/gpurun_out/dgather_$tag.txt PS_TRACE_REQUESTS=$PWD/gpurun_out/dtrace_$tag.txt step 200 tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 30 5 "$dl" > gpurun_out/dtrace_$tag.log 2>&1; echo "$st rc=$?"; grep "^{" gpurun_out/dtrace_$tag.log | cut -c1-300
           python3 tools/run_sizes.py gpurun_out/dtrace_$tag.txt ;;
     dprof:*)
           # dprof:N:mode:layout — rocprof kernel stats + trace of kv_bench_dropin
