@@ -45,6 +45,18 @@ def test_svector_semantics():
     assert "svector ok" in r.stdout
 
 
+def test_receive_queue_conditional_pop():
+    """The receive queue's PopIf (internal/customer.h), which the servers'
+    gather window relies on: an empty queue is no refusal, a rejected head is,
+    a message pushed while a consumer polls is taken (never reported as a
+    refusal), and messages leave in priority then arrival order."""
+    exe = os.path.join(BIN, "queue_unit")
+    _need(exe)
+    r = run(exe)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "queue ok" in r.stdout
+
+
 def test_shm_frame_arena():
     """The process-mode frame arena (src/shm_pool.cc): live frames never
     overlap under random churn, freed ranges coalesce, a full arena and an
