@@ -152,7 +152,7 @@ PY
           # step reach a server spread out and, with the default window, fewer
           # runs form than in the unprofiled line)
           IFS=: read -r _ dn dm <<< "$st"; tag="n${dn}_${dm}"; o=gpurun_out/pmc_dropin_$tag; rm -rf "$o"; mkdir -p "$o"
-          export PS_RUN_GATHER_US=${PMC_GATHER_US:-120}
+          export PS_RUN_GATHER_US=${PMC_GATHER_US:-120} PS_RUN_GATHER_ORD_US=${PMC_GATHER_ORD_US:-1000}
           md=""; [ "$dm" = procs ] && md="-procs"
           for sN in 10 40; do for c in FETCH_SIZE WRITE_SIZE; do
             step 240 rocprofv3 --pmc $c --output-format csv -d "$o/$c.$sN" -- tests/_bin/kv_bench_dropin -ns "$dn" -nw "$dn" $md 10000000 $sN 5 0 > "$o/$c.$sN.log" 2>&1 || { echo "pmcdropin pass $c $sN failed"; exit 1; }
