@@ -521,20 +521,32 @@ class KVServer : public SimpleApp {
   // requests taken from each sender so far (a request's ordinal: the n-th from
   // its sender)
   std::unordered_map<int, uint64_t> taken_;
-  uint64_t Take(int sender) { return ++taken_[sender]; }
+  // senders a window timed out waiting for: not waited for again until they
+  // send (a worker that skips this server, or has stopped)
+  std::unordered_map<int, bool> stalled_;
+  uint64_t Take(int sender) {
+    stalled_.erase(sender);
+    return ++taken_[sender];
+  }
   // a recent sender outside the run that this server has taken fewer than m
-  // requests from (its next request is the run's round or an earlier one)
-  bool SendersBehind(const std::vector<KVRunItem<Value>>& items, uint64_t m) {
+  // requests from (its next request is the run's round or an earlier one);
+  // mark: note every such sender as stalled instead
+  bool SendersBehind(const std::vector<KVRunItem<Value>>& items, uint64_t m, bool mark = false) {
     const unsigned n = recent_n_ < 64 ? recent_n_ : 64;
+    bool any = false;
     for (unsigned i = 0; i < n; ++i) {
       const int w = recent_[i];
       bool in = false;
       for (const auto& it : items) in = in || it.meta.sender == w;
-      if (in) continue;
+      if (in || stalled_.count(w)) continue;
       auto t = taken_.find(w);
-      if ((t == taken_.end() ? 0 : t->second) < m) return true;
+      if ((t == taken_.end() ? 0 : t->second) < m) {
+        if (!mark) return true;
+        stalled_[w] = true;
+        any = true;
+      }
     }
-    return false;
+    return any;
   }
   void NoteSender(int sender) { recent_[recent_n_++ & 63] = sender; }
   size_t RecentSenders(int sender) {
@@ -1016,6 +1028,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
           break;
         }
         if (std::chrono::steady_clock::now() - t_gather > std::chrono::microseconds(gather_us)) {
+          if (by_ordinal) (void)SendersBehind(items, low, true);
           if (!waited && ++gather_idle_ >= 4) {
             gather_idle_ = 0;
             gather_cool_ = 64;
