@@ -351,6 +351,16 @@ int psg_store_push_frames(psg_store* s, const uint64_t* const* keys_host, uint64
 #define PSG_RUN_STRIDED 2
 int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
                   const void* const* vals, void* const* outs, psg_stream stream, int* served);
+/* psg_store_run with a status per request (status: k ints): a request whose
+ * key lies outside the store's range is refused on its own (status
+ * PSG_ERR_RANGE, nothing of it applied) and the others are served, in order.
+ * Returns PSG_OK when every request was served or refused that way; any other
+ * failure stops the run (the failing request and those after it carry its
+ * code).  The server's answer to a worker's unconfirmed slice
+ * (KVWorker::Send, Meta::spec_slice): a wrong one is refused, not applied. */
+int psg_store_run_status(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
+                         const void* const* vals, void* const* outs, psg_stream stream, int* served,
+                         int* status);
 
 /* The stable device radix sort of the order-preserving path (psg_sort.hip),
  * exported for its parity tests: sorts (keys[i], vals[i]) by bits [0, bits) of
@@ -436,6 +446,15 @@ int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_va
               int num_servers, const uint64_t* begins_host,
               const uint64_t* ends_host, uint64_t* key_pos_host,
               uint64_t* val_pos_host, psg_stream stream);
+
+/* The bounds psg_slice found at its last slice of this key array (same
+ * pointer, n, server count and first range) on this thread, without reading
+ * the keys: *found = 1 and key_pos_host (ns + 1 entries) filled, else
+ * *found = 0.  A worker may send these slices unconfirmed when every server
+ * checks each key against its own range (a wrong bound puts some key outside
+ * its server's range, and that server refuses the request). */
+int psg_slice_hint(const uint64_t* keys, uint64_t n, int num_servers, uint64_t begin0, uint64_t* key_pos_host,
+                   int* found);
 
 /* One pull reply (KVPairs from one server, KVApp.h:631-637). */
 typedef struct psg_segment {

@@ -286,6 +286,9 @@ struct psg_store {
   int run_last;       // PSG_RUN_* the last run was served as
   uint32_t run_fail_gen;  // K's generation at which a run with Pulls was not strided
   int run_fail_count;     // ... and how many runs since were served one by one without trying
+  // psg_store_run_status: per-request codes of a run served one by one (a
+  // request refused for a key outside the range does not stop the run)
+  int* run_status = nullptr;
 };
 
 struct psg_adam {

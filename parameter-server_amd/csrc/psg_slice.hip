@@ -193,6 +193,23 @@ int psg_server_ranges(int num_servers, uint64_t* begins_host, uint64_t* ends_hos
   return PSG_OK;
 }
 
+int psg_slice_hint(const uint64_t* keys, uint64_t n, int num_servers, uint64_t begin0, uint64_t* key_pos_host,
+                   int* found) {
+  PSG_REQUIRE(found && key_pos_host && num_servers > 0, PSG_ERR_INVALID, "psg_slice_hint: bad arguments");
+  *found = 0;
+  const int nb = num_servers + 1;
+  SliceScratch* sc = nullptr;
+  PSG_TRY(get_slice_scratch(nb, &sc));
+  for (auto& l : sc->last)
+    if (l.keys == keys && l.n == n && l.nb == nb && l.begin0 == begin0 && (int)l.pos.size() == nb) {
+      for (int i = 0; i < nb; ++i) key_pos_host[i] = l.pos[i];
+      l.use = ++sc->clock;
+      *found = 1;
+      break;
+    }
+  return PSG_OK;
+}
+
 int psg_slice(const uint64_t* keys, uint64_t n, const int* lens, uint64_t num_vals, int num_servers,
               const uint64_t* begins_host, const uint64_t* ends_host, uint64_t* key_pos_host,
               uint64_t* val_pos_host, psg_stream stream) {

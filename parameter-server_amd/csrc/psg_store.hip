@@ -3249,10 +3249,20 @@ static bool frames_on() {
 
 // The k requests one after the other, each to completion: the reference's
 // sequence, and the fallback of every run the one-pass forms do not cover.
+// (psg_store_run_status: a request refused for a key outside the range is
+// recorded and the run goes on; any other failure stops it)
+static int one_status(psg_store* s, int k, int j, int rc) {
+  if (!s->run_status || rc == PSG_OK) return rc;
+  s->run_status[j] = rc;
+  if (rc == PSG_ERR_RANGE) return PSG_OK;
+  for (int i = j + 1; i < k; ++i) s->run_status[i] = rc;
+  return rc;
+}
+
 static int frames_one_by_one(psg_store* s, const uint64_t* const* keys, uint64_t first_key,
                              const void* const* vals, int k, uint64_t n, hipStream_t st) {
   for (int j = 0; j < k; ++j)
-    PSG_TRY(handle_sync(s, PSG_PUSH, keys ? keys[j] : nullptr, first_key, vals[j], nullptr, n, st));
+    PSG_TRY(one_status(s, k, j, handle_sync(s, PSG_PUSH, keys ? keys[j] : nullptr, first_key, vals[j], nullptr, n, st)));
   return PSG_OK;
 }
 
@@ -3312,8 +3322,9 @@ static bool strided_on() {
 static int run_one_by_one(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
                           const void* const* vals, void* const* outs, hipStream_t st) {
   for (int j = 0; j < k; ++j)
-    PSG_TRY(handle_sync(s, ops[j], keys[j], 0, (ops[j] & PSG_PUSH) ? vals[j] : nullptr,
-                        (ops[j] & PSG_PULL) ? outs[j] : nullptr, ns[j], st));
+    PSG_TRY(one_status(s, k, j,
+                       handle_sync(s, ops[j], keys[j], 0, (ops[j] & PSG_PUSH) ? vals[j] : nullptr,
+                                   (ops[j] & PSG_PULL) ? outs[j] : nullptr, ns[j], st)));
   return PSG_OK;
 }
 
@@ -3859,6 +3870,24 @@ int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* ke
   if (k > 1) s->run_last = sv;
   if (served) *served = sv;
   return PSG_OK;
+}
+
+int psg_store_run_status(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
+                         const void* const* vals, void* const* outs, psg_stream stream, int* served, int* status) {
+  PSG_REQUIRE(s && status && k >= 1 && k <= kMaxFrames, PSG_ERR_INVALID, "psg_store_run_status: bad arguments");
+  for (int j = 0; j < k; ++j) status[j] = PSG_OK;
+  s->run_status = status;
+  const int rc = psg_store_run(s, k, ops, keys, ns, vals, outs, stream, served);
+  s->run_status = nullptr;
+  if (rc != PSG_OK) {
+    // a failure one_status did not record (an argument check, a launch of a
+    // one-pass form) applied nothing: every request carries it
+    bool recorded = false;
+    for (int j = 0; j < k; ++j) recorded = recorded || status[j] != PSG_OK;
+    if (!recorded)
+      for (int j = 0; j < k; ++j) status[j] = rc;
+  }
+  return rc;
 }
 
 int psg_store_push_slots_frames(psg_store* s, const uint32_t* slots, uint64_t first, const void* const* vals_host,

@@ -113,6 +113,9 @@ class Customer {
   void WaitRequest(int request_id);
   int GetResponse(int request_id);
   void AddResponse(int request_id, int cnt = 1);
+  /* cnt more responses to wait for (a request re-sent in pieces) */
+  void ExpectMore(int request_id, int cnt);
+  int NumExpected(int request_id);
   /* called by the Van for every data message to this customer */
   void OnReceive(const Message& received) { receive_queue_.Push(received); }
   /* From the receive thread's handle: take the next queued message if take(it)

@@ -77,6 +77,13 @@ struct Meta {
   // request: a Pull whose frame 1 is the caller's HBM output slice (the server
   // may write the values there); reply: it did, and carries no values
   bool direct_reply = false;
+  // request: its slice bounds are the worker's hint from the last slice of
+  // this key array, not confirmed (the servers' own checks confirm them);
+  // reply: the server's handle checks every slice it is sent (may be sent one)
+  bool spec_slice = false;
+  // reply: a speculative slice this server refused (a key outside its range;
+  // nothing applied) — the worker re-sends its keys sliced for real
+  bool refused = false;
   std::string body;
   std::vector<DataType> data_type;
   Control control;

@@ -220,6 +220,16 @@ inline void TraceRequest(int server, const KVMeta& m, size_t keys, size_t run_si
   if (len > 0) (void)!::write(fd, line, (size_t)len);
 }
 
+/* PS_SPEC_SLICE=1: a worker sends an HBM key list it sliced before on the
+ * bounds it had then, unconfirmed, when every server checks its slices
+ * (KVWorker::Send; default 0). */
+inline bool SpecSliceOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_SPEC_SLICE");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
 /* PS_TRACE_GATHER=<file> (diagnostics): one line per gathered run, "server
  * head_sender head_ordinal run_size why waited_us" — why the gather ended:
  * 0 run full, 1 no sender behind (or no window), 2 a queued message that
@@ -372,7 +382,10 @@ class KVWorker : public SimpleApp {
     return ts;
   }
 
+  /* slices its servers refused (Refused; PS_SPEC_SLICE) */
+  uint64_t refused_slices() const { return refused_.load(); }
   void set_slicer(const Slicer& slicer) {
+    default_slicer_ = false;
     CHECK(static_cast<bool>(slicer));
     slicer_ = slicer;
   }
@@ -397,6 +410,38 @@ class KVWorker : public SimpleApp {
   std::vector<char> hbm_server_;
   int hbm_count_ = 0;
   std::atomic<bool> servers_take_hbm_{false};
+  // servers whose handle takes unconfirmed slices (Meta::spec_slice in their
+  // replies); all of them: the worker may send the slicer's hints unconfirmed
+  void NoteSpecServer(int sender) {
+    std::lock_guard<std::mutex> lk(mu_);
+    const int ns = PostOffice::Get()->num_servers();
+    if (spec_server_.size() != (size_t)ns) spec_server_.assign(ns, 0);
+    const int r = PostOffice::IDToRank(sender);
+    if (r < ns && !spec_server_[r]) {
+      spec_server_[r] = 1;
+      if (++spec_count_ == ns) servers_take_spec_ = true;
+    }
+  }
+  std::vector<char> spec_server_;
+  int spec_count_ = 0;
+  std::atomic<bool> servers_take_spec_{false};
+  // a request sent on unconfirmed slices: what a refusal needs to re-send
+  struct SpecSend {
+    bool push = false, pull = false, direct = false, has_outs = false;
+    int cmd = 0;
+    Data kvs;
+    SVector<Value> outs;
+    std::vector<uint64_t> pos;  // the hinted key bounds, num_servers + 1
+  };
+  std::unordered_map<int, SpecSend> spec_sends_;
+  std::unordered_map<const void*, bool> spec_stale_;  // key arrays a refusal proved re-sliced since
+  bool default_slicer_ = true;
+  std::atomic<uint64_t> refused_{0};
+  void SendOne(int timestamp, bool push, bool pull, int cmd, int priority, const Data& whole, const Data& kv,
+               bool direct, const SVector<Value>* outs, int server_rank, bool spec);
+  void Refused(const Message& msg);
+  void SendPieces(int timestamp, const SpecSend& sp, uint64_t a, uint64_t b, const std::vector<uint64_t>& pos,
+                  int* sent);
 
   void AddCallback(int timestamp, const Callback& cb) {
     if (!cb) return;
@@ -425,6 +470,7 @@ struct KVRunItem {
   KVMeta meta;
   KVPairs<Value> data;
   SVector<Value> out;  // the output slice a Pull offered for its reply (direct reply), else empty
+  bool spec = false;   // its slice is the worker's unconfirmed hint (Meta::spec_slice)
 };
 
 template <typename Value>
@@ -467,6 +513,15 @@ class KVServer : public SimpleApp {
    * wrote the Pull's values into the output slice the request offered
    * (KVRunItem::out), so the reply carries its keys and no values. */
   void RunResponse(const KVMeta& req, const KVPairs<Value>& res, bool direct) { Reply(req, res, direct); }
+  /* For a run handle: refuse a request whose unconfirmed slice (KVRunItem::spec)
+   * holds a key outside this server's range — nothing of it was applied; the
+   * worker re-sends its keys sliced for real. */
+  void RunRefuse(const KVMeta& req) { Reply(req, KVPairs<Value>(), false, true); }
+  /* this server takes unconfirmed slices: its handle checks every key of a run
+   * against its own range and refuses a wrong slice instead of failing */
+  bool TakesSpecSlices() const {
+    return static_cast<bool>(run_handle_) && device_frames_.load() && detail::PushRunsOn() && detail::MixedRunsOn();
+  }
   /* For a run handle: serve one request of a run with the installed handle, as
    * if it had been taken on its own (its output offer included). */
   void ServeOne(const KVRunItem<Value>& item) {
@@ -481,7 +536,7 @@ class KVServer : public SimpleApp {
 
  private:
   void OnReceive(const Message& msg) override;
-  void Reply(const KVMeta& req, const KVPairs<Value>& res, bool direct);
+  void Reply(const KVMeta& req, const KVPairs<Value>& res, bool direct, bool refused = false);
   void Install(const ReqHandle& h, bool device_frames, const RunHandle& run = nullptr) {
     {
       std::lock_guard<std::mutex> lk(handle_mu_);
@@ -706,11 +761,13 @@ struct KVServerDefaultHandle {
     if (all_push) {
       std::vector<KVMeta> metas;
       std::vector<KVPairs<Value>> datas;
+      std::vector<char> spec;
       for (const auto& it : run) {
         metas.push_back(it.meta);
         datas.push_back(it.data);
+        spec.push_back(it.spec ? 1 : 0);
       }
-      PushRun(metas, datas, server);
+      PushRun(metas, datas, server, spec);
       return;
     }
     if (state->key_cache && hashed) {
@@ -752,18 +809,28 @@ struct KVServerDefaultHandle {
         op[j] = douts[j].data();
       }
     }
+    std::vector<int> status(k, PSG_OK);
     {
       stage::Scope t("server.handle.store.run");
       int served = 0;
-      device::Check(psg_store_run(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), op.data(), s,
-                                  &served),
-                    "psg_store_run");
+      const int rc = psg_store_run_status(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(),
+                                          op.data(), s, &served, status.data());
+      if (rc != PSG_OK) device::Check(rc, "psg_store_run");
     }
+    // a request refused for a key outside this shard: fatal, as a CHECK,
+    // unless its slice was the worker's unconfirmed hint
+    for (size_t j = 0; j < k; ++j)
+      if (status[j] != PSG_OK && !run[j].spec) device::Check(status[j], "psg_store_run");
     if (state->key_cache)
       for (size_t j = 0; j < k; ++j)
-        Remember(dkeys[j], run[j].data.keys.on_device(),
-                 run[j].data.keys.on_device() ? 0 : detail::KeyListHash(run[j].data.keys.data(), ns[j]), s);
+        if (status[j] == PSG_OK)
+          Remember(dkeys[j], run[j].data.keys.on_device(),
+                   run[j].data.keys.on_device() ? 0 : detail::KeyListHash(run[j].data.keys.data(), ns[j]), s);
     for (size_t j = 0; j < k; ++j) {
+      if (status[j] != PSG_OK) {
+        server->RunRefuse(run[j].meta);
+        continue;
+      }
       KVPairs<Value> res;
       if (run[j].meta.pull) {
         res.keys = run[j].data.keys;
@@ -774,7 +841,9 @@ struct KVServerDefaultHandle {
   }
 
   /* A run of Pushes of one shape (Run). */
-  void PushRun(const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& datas, KVServer<Value>* server) {
+  void PushRun(const std::vector<KVMeta>& metas, const std::vector<KVPairs<Value>>& datas, KVServer<Value>* server,
+               const std::vector<char>& spec = {}) {
+    std::vector<int> status(datas.size(), PSG_OK);
     const int dev = PostOffice::Get()->device();
     CHECK_GE(dev, 0) << "KVServerDefaultHandle: the value store lives in HBM and this node has no GPU";
     constexpr int dt = device::DType<Value>();
@@ -830,15 +899,21 @@ struct KVServerDefaultHandle {
       std::vector<int> ops(k, PSG_PUSH);
       std::vector<uint64_t> ns(k, n);
       int served = 0;
-      device::Check(psg_store_run(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), nullptr, s,
-                                  &served),
-                    "psg_store_run");
+      const int rc = psg_store_run_status(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), nullptr,
+                                          s, &served, status.data());
+      if (rc != PSG_OK) device::Check(rc, "psg_store_run");
+      for (size_t j = 0; j < k; ++j)
+        if (status[j] != PSG_OK && !(j < spec.size() && spec[j])) device::Check(status[j], "psg_store_run");
       if (state->key_cache)
         for (size_t j = 0; j < k; ++j)
-          Remember(dkeys[j], datas[j].keys.on_device(),
-                   datas[j].keys.on_device() ? 0 : detail::KeyListHash(datas[j].keys.data(), n), s);
+          if (status[j] == PSG_OK)
+            Remember(dkeys[j], datas[j].keys.on_device(),
+                     datas[j].keys.on_device() ? 0 : detail::KeyListHash(datas[j].keys.data(), n), s);
     }
-    for (const KVMeta& m : metas) server->Response(m, KVPairs<Value>());
+    for (size_t j = 0; j < metas.size(); ++j) {
+      if (status[j] != PSG_OK) server->RunRefuse(metas[j]);
+      else server->Response(metas[j], KVPairs<Value>());
+    }
   }
 
   psg_store* store() const { return state->store; }
@@ -984,6 +1059,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
     items[0].meta = meta;
     items[0].data = data;
     items[0].out = direct_out_;
+    items[0].spec = msg.meta.spec_slice;
     auto mate = [&](const Message& m) {
       if (m.meta.app_id != msg.meta.app_id || !PlainRequest(m)) return false;
       if (all_push && push_shape(m)) return true;
@@ -1052,6 +1128,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       it.data.keys = next.data[0];
       if (next.meta.push) it.data.vals = next.data[1];
       if (next.meta.direct_reply) it.out = next.data[next.data.size() - 1];
+      it.spec = next.meta.spec_slice;
       items.push_back(std::move(it));
     }
     // (a plain request on its own goes to the run handle too: the store
@@ -1070,6 +1147,7 @@ void KVServer<Value>::OnReceive(const Message& msg) {
       return;
     }
   }
+  CHECK(!msg.meta.spec_slice) << "an unconfirmed slice reached a handle that does not check it";
   detail::TraceRequest(PostOffice::Get()->my_id(), meta, data.keys.size(), 1, 0);
   // called in place: a handle keeps its state across requests (KVApp.h:457)
   {
@@ -1088,7 +1166,7 @@ void KVServer<Value>::Response(const KVMeta& req, const KVPairs<Value>& res) {
 }
 
 template <typename Value>
-void KVServer<Value>::Reply(const KVMeta& req, const KVPairs<Value>& res, bool direct) {
+void KVServer<Value>::Reply(const KVMeta& req, const KVPairs<Value>& res, bool direct, bool refused) {
   stage::Scope t("server.response", res.keys.size() * sizeof(Key) + res.vals.size() * sizeof(Value));
   Message msg;
   msg.meta.app_id = customer_->app_id();
@@ -1103,6 +1181,10 @@ void KVServer<Value>::Reply(const KVMeta& req, const KVPairs<Value>& res, bool d
   msg.meta.hbm_handle = device_frames_.load();
   msg.meta.direct_reply = direct;
   if (msg.meta.direct_reply) CHECK(res.vals.empty()) << "a direct reply carries no values";
+  // tells the worker it may send this server unconfirmed slices (KVWorker::Send)
+  msg.meta.spec_slice = TakesSpecSlices();
+  msg.meta.refused = refused;
+  if (refused) CHECK(res.keys.empty() && !direct) << "a refusal carries nothing";
   if (res.keys.size()) {
     msg.AddData(res.keys);
     msg.AddData(res.vals);
@@ -1182,65 +1264,169 @@ void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const D
                            const SVector<Value>* outs) {
   stage::Scope t_send(push ? "worker.send.push" : "worker.send.pull");
   SlicedKVs sliced;
-  slicer_(const_cast<Data&>(kvs), PostOffice::Get()->GetServerRanges(), &sliced);
+  const std::vector<Range>& ranges = PostOffice::Get()->GetServerRanges();
+  const size_t ns = ranges.size();
+  // Unconfirmed slices (PS_SPEC_SLICE): an HBM key list this thread sliced
+  // before is sent on the bounds it had then, without the slicer's kernel and
+  // readback, when every server's handle checks each key against its own
+  // range (a wrong bound puts some key outside its server's range; that
+  // server refuses its slice, applying nothing, and Refused re-sends those
+  // keys sliced for real).  Not with lens, a custom slicer, or a Pull merged
+  // on the host (its replies must be the servers' slices).
+  bool spec = false;
+  std::vector<uint64_t> hint;
+  const size_t nkeys = kvs.keys.size();
+  if (detail::SpecSliceOn() && default_slicer_ && ns > 1 && nkeys && kvs.keys.on_device() && kvs.lens.empty() &&
+      (!pull || direct) && servers_take_spec_.load()) {
+    bool stale = false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stale = spec_stale_.erase(kvs.keys.data()) > 0;
+    }
+    int found = 0;
+    hint.assign(ns + 1, 0);
+    if (!stale)
+      device::Check(psg_slice_hint(kvs.keys.data(), nkeys, (int)ns, ranges[0].begin, hint.data(), &found),
+                    "psg_slice_hint");
+    if (found && hint[ns] == nkeys) {
+      const size_t per = kvs.vals.size() / nkeys;
+      CHECK_EQ(per * nkeys, kvs.vals.size());
+      sliced.resize(ns);
+      for (size_t i = 0; i < ns; ++i) {
+        auto& sl = sliced[i];
+        sl.first = hint[i + 1] != hint[i];
+        if (!sl.first) continue;
+        sl.second.keys = kvs.keys.Slice(hint[i], hint[i + 1]);
+        sl.second.vals = kvs.vals.Slice(hint[i] * per, hint[i + 1] * per);
+      }
+      spec = true;
+      SpecSend sp;
+      sp.push = push;
+      sp.pull = pull;
+      sp.direct = direct;
+      sp.cmd = cmd;
+      sp.kvs = kvs;
+      sp.has_outs = outs != nullptr;
+      if (outs) sp.outs = *outs;
+      sp.pos = hint;
+      std::lock_guard<std::mutex> lk(mu_);
+      spec_sends_[timestamp] = std::move(sp);
+    }
+  }
+  if (!spec) slicer_(const_cast<Data&>(kvs), ranges, &sliced);
   int skipped = 0;
-  for (auto& s : sliced)
-    if (!s.first) ++skipped;
+  for (auto& sl : sliced)
+    if (!sl.first) ++skipped;
   customer_->AddResponse(timestamp, skipped);
   if ((size_t)skipped == sliced.size()) RunCallback(timestamp);
   for (size_t i = 0; i < sliced.size(); ++i) {
-    const auto& s = sliced[i];
-    if (!s.first) continue;
-    Message msg;
-    msg.meta.app_id = customer_->app_id();
-    msg.meta.customer_id = customer_->customer_id();
-    msg.meta.request = true;
-    msg.meta.push = push;
-    msg.meta.pull = pull;
-    msg.meta.head = cmd;
-    msg.meta.timestamp = timestamp;
-    msg.meta.receiver = PostOffice::ServerRankToID((int)i);
-    msg.meta.priority = kvs.priority;
-    msg.meta.direct_reply = direct;
-    const auto& kv = s.second;
-    SVector<Value> out_slice;
-    if (direct && outs) {
-      // a PushPull: the output slice at this server's values' offset, found
-      // from where its vals slice sits in the request (a slicer that copied
-      // the values instead of slicing them gets no offer)
-      const Value* base = kvs.vals.data();
-      const Value* v = kv.vals.data();
-      if (kv.vals.size() && v >= base && v + kv.vals.size() <= base + kvs.vals.size()) {
-        const size_t off = (size_t)(v - base);
-        out_slice = outs->Slice(off, off + kv.vals.size());
-      } else {
-        msg.meta.direct_reply = false;
-      }
+    if (!sliced[i].first) continue;
+    SendOne(timestamp, push, pull, cmd, kvs.priority, kvs, sliced[i].second, direct, outs, (int)i, spec);
+  }
+}
+
+// One server's slice of a request (Send, SendPieces): `kv` is a slice of
+// `whole`, the request as the caller gave it.
+template <typename Value>
+void KVWorker<Value>::SendOne(int timestamp, bool push, bool pull, int cmd, int priority, const Data& whole,
+                              const Data& kv, bool direct, const SVector<Value>* outs, int server_rank, bool spec) {
+  Message msg;
+  msg.meta.app_id = customer_->app_id();
+  msg.meta.customer_id = customer_->customer_id();
+  msg.meta.request = true;
+  msg.meta.push = push;
+  msg.meta.pull = pull;
+  msg.meta.head = cmd;
+  msg.meta.timestamp = timestamp;
+  msg.meta.receiver = PostOffice::ServerRankToID(server_rank);
+  msg.meta.priority = priority;
+  msg.meta.direct_reply = direct;
+  msg.meta.spec_slice = spec;
+  SVector<Value> out_slice;
+  if (direct && outs) {
+    // a PushPull: the output slice at this server's values' offset, found
+    // from where its vals slice sits in the request (a slicer that copied
+    // the values instead of slicing them gets no offer)
+    const Value* base = whole.vals.data();
+    const Value* v = kv.vals.data();
+    if (kv.vals.size() && v >= base && v + kv.vals.size() <= base + whole.vals.size()) {
+      const size_t off = (size_t)(v - base);
+      out_slice = outs->Slice(off, off + kv.vals.size());
+    } else {
+      msg.meta.direct_reply = false;
     }
-    bool drop_vals = false;
-    if (direct && !outs) {
-      // a Pull whose vals frame is the caller's output: offered only when this
-      // server's vals slice is the output at its keys' offset (a custom slicer
-      // that copied or remapped the values gets no offer, and a plain Pull
-      // request without values, as the reference sends)
-      const Key* kbase = kvs.keys.data();
-      const Key* k = kv.keys.data();
-      const size_t per = kvs.keys.size() ? kvs.vals.size() / kvs.keys.size() : 0;
-      const bool keys_inside = kv.keys.size() && k >= kbase && k + kv.keys.size() <= kbase + kvs.keys.size();
-      const bool ok = keys_inside && per && kv.vals.size() == kv.keys.size() * per &&
-                      kv.vals.data() == kvs.vals.data() + (size_t)(k - kbase) * per;
-      if (!ok) {
-        msg.meta.direct_reply = false;
-        drop_vals = true;
-      }
+  }
+  bool drop_vals = false;
+  if (direct && !outs) {
+    // a Pull whose vals frame is the caller's output: offered only when this
+    // server's vals slice is the output at its keys' offset (a custom slicer
+    // that copied or remapped the values gets no offer, and a plain Pull
+    // request without values, as the reference sends)
+    const Key* kbase = whole.keys.data();
+    const Key* k = kv.keys.data();
+    const size_t per = whole.keys.size() ? whole.vals.size() / whole.keys.size() : 0;
+    const bool keys_inside = kv.keys.size() && k >= kbase && k + kv.keys.size() <= kbase + whole.keys.size();
+    const bool ok = keys_inside && per && kv.vals.size() == kv.keys.size() * per &&
+                    kv.vals.data() == whole.vals.data() + (size_t)(k - kbase) * per;
+    if (!ok) {
+      msg.meta.direct_reply = false;
+      drop_vals = true;
     }
-    if (kv.keys.size()) {
-      msg.AddData(kv.keys);
-      msg.AddData(drop_vals ? SVector<Value>() : kv.vals);
-      if (kv.lens.size()) msg.AddData(kv.lens);
-      if (msg.meta.direct_reply && outs) msg.AddData(out_slice);
-    }
-    PostOffice::Get()->van()->Send(msg);
+  }
+  if (kv.keys.size()) {
+    msg.AddData(kv.keys);
+    msg.AddData(drop_vals ? SVector<Value>() : kv.vals);
+    if (kv.lens.size()) msg.AddData(kv.lens);
+    if (msg.meta.direct_reply && outs) msg.AddData(out_slice);
+  }
+  PostOffice::Get()->van()->Send(msg);
+}
+
+// A server refused its unconfirmed slice [pos[r], pos[r+1]) of request
+// `timestamp` (a key outside its range: the key list changed since it was
+// last sliced; nothing of that slice was applied).  The list is sliced for
+// real and those keys go to the servers that own them, as requests of the same
+// timestamp; the request now waits for their replies too.  The servers that
+// took their slices hold exactly their keys (each accepted slice lies in its
+// server's range), so every key is still applied once.
+template <typename Value>
+void KVWorker<Value>::Refused(const Message& msg) {
+  const int ts = msg.meta.timestamp;
+  ++refused_;
+  SpecSend sp;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = spec_sends_.find(ts);
+    CHECK(it != spec_sends_.end()) << "a refusal of request " << ts << ", which was not sent on unconfirmed slices";
+    sp = it->second;
+    spec_stale_[sp.kvs.keys.data()] = true;  // the sender's thread slices it for real next time
+  }
+  const int r = PostOffice::IDToRank(msg.meta.sender);
+  const std::vector<Range>& ranges = PostOffice::Get()->GetServerRanges();
+  CHECK_LT((size_t)r + 1, sp.pos.size());
+  std::vector<uint64_t> pos, vpos;
+  device::SliceKeys(sp.kvs.keys.data(), sp.kvs.keys.size(), nullptr, sp.kvs.vals.size(), ranges, &pos, &vpos);
+  int sent = 0;
+  SendPieces(ts, sp, sp.pos[r], sp.pos[r + 1], pos, &sent);
+  // (before this reply is counted: the request now waits for `sent` more)
+  customer_->ExpectMore(ts, sent);
+}
+
+template <typename Value>
+void KVWorker<Value>::SendPieces(int timestamp, const SpecSend& sp, uint64_t a, uint64_t b,
+                                 const std::vector<uint64_t>& pos, int* sent) {
+  const size_t n = sp.kvs.keys.size();
+  const size_t per = n ? sp.kvs.vals.size() / n : 0;
+  *sent = 0;
+  for (size_t i = 0; i + 1 < pos.size(); ++i) {
+    const uint64_t lo = std::max<uint64_t>(a, pos[i]), hi = std::min<uint64_t>(b, pos[i + 1]);
+    if (lo >= hi) continue;
+    Data kv;
+    kv.keys = sp.kvs.keys.Slice(lo, hi);
+    kv.vals = sp.kvs.vals.Slice(lo * per, hi * per);
+    SendOne(timestamp, sp.push, sp.pull, sp.cmd, sp.kvs.priority, sp.kvs, kv, sp.direct,
+            sp.has_outs ? &sp.outs : nullptr, (int)i, false);
+    ++*sent;
   }
 }
 
@@ -1252,6 +1438,11 @@ void KVWorker<Value>::OnReceive(const Message& msg) {
   }
   const int ts = msg.meta.timestamp;
   if (msg.meta.hbm_handle && !servers_take_hbm_.load()) NoteHbmServer(msg.meta.sender);
+  if (msg.meta.spec_slice && !servers_take_spec_.load()) NoteSpecServer(msg.meta.sender);
+  if (msg.meta.refused) {
+    Refused(msg);
+    return;  // (counted as a reply; the re-sent pieces are waited for)
+  }
   if (msg.meta.pull) {
     CHECK_GE(msg.data.size(), (size_t)2);
     Reply r;
@@ -1264,7 +1455,13 @@ void KVWorker<Value>::OnReceive(const Message& msg) {
     recv_kvs_[ts].push_back(std::move(r));
   }
   // the tracker is bumped after this handle returns (Customer.cpp:58-67)
-  if (customer_->GetResponse(ts) == PostOffice::Get()->num_servers() - 1) RunCallback(ts);
+  if (customer_->GetResponse(ts) == customer_->NumExpected(ts) - 1) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      spec_sends_.erase(ts);
+    }
+    RunCallback(ts);
+  }
 }
 
 template <typename Value>

@@ -73,6 +73,16 @@ int Customer::GetResponse(int request_id) {
   return tracker_[request_id].second;
 }
 
+void Customer::ExpectMore(int request_id, int cnt) {
+  std::lock_guard<std::mutex> lk(tracker_mu_);
+  tracker_[request_id].first += cnt;
+}
+
+int Customer::NumExpected(int request_id) {
+  std::lock_guard<std::mutex> lk(tracker_mu_);
+  return tracker_[request_id].first;
+}
+
 void Customer::AddResponse(int request_id, int cnt) {
   std::lock_guard<std::mutex> lk(tracker_mu_);
   tracker_[request_id].second += cnt;

@@ -447,7 +447,7 @@ void PutMeta(Writer& w, const Meta& m) {
   w.pod<int32_t>(m.sender);
   w.pod<int32_t>(m.receiver);
   w.pod<uint8_t>((uint8_t)(m.request | (m.push << 1) | (m.pull << 2) | (m.simple_app << 3) | (m.hbm_handle << 4) |
-                           (m.direct_reply << 5)));
+                           (m.direct_reply << 5) | (m.spec_slice << 6) | (m.refused << 7)));
   w.str(m.body);
   w.pod<uint32_t>((uint32_t)m.data_type.size());
   for (DataType t : m.data_type) w.pod<int32_t>((int32_t)t);
@@ -475,6 +475,8 @@ Meta GetMeta(Reader& r) {
   m.simple_app = (f >> 3) & 1;
   m.hbm_handle = (f >> 4) & 1;
   m.direct_reply = (f >> 5) & 1;
+  m.spec_slice = (f >> 6) & 1;
+  m.refused = (f >> 7) & 1;
   m.body = r.str();
   const uint32_t nt = r.pod<uint32_t>();
   for (uint32_t i = 0; i < nt; ++i) m.data_type.push_back((DataType)r.pod<int32_t>());
