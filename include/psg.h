@@ -361,6 +361,11 @@ int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* ke
 int psg_store_run_status(psg_store* s, int k, const int* ops, const uint64_t* const* keys, const uint64_t* ns,
                          const void* const* vals, void* const* outs, psg_stream stream, int* served,
                          int* status);
+/* A SORTED store's key range from now on (psg_store_create's key_begin /
+ * key_end): a request key outside it rejects the request, on every path (the
+ * strided pass checks it too).  The default handle narrows it to the server's
+ * own range while it serves unconfirmed slices, then widens it again. */
+int psg_store_set_key_range(psg_store* s, uint64_t key_begin, uint64_t key_end);
 
 /* The stable device radix sort of the order-preserving path (psg_sort.hip),
  * exported for its parity tests: sorts (keys[i], vals[i]) by bits [0, bits) of

@@ -372,6 +372,7 @@ struct RunFrames {
   void* o[kMaxFrames];            // its reply values (PSG_PULL)
   uint64_t n[kMaxFrames];         // its keys
   int op[kMaxFrames];             // PSG_PUSH | PSG_PULL bits
+  uint64_t lo, hi;                // the store's key range: a key outside it fails the check
 };
 // run_classify: one block; from the requests' first keys (and the second key of
 //   request pl, which gives P) writes *desc and *seen (pinned host); *same_base

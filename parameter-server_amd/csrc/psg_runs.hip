@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void k_run_pass(typename Elem<DT>::T* __restri
       if constexpr (MODE != RUN_APPLY) {
 #pragma unroll
         for (int e = 0; e < V; ++e)
-          if (ops[u][e] && qq[u][e] != kk[u][e]) mismatch = 1;
+          if (ops[u][e] && (qq[u][e] != kk[u][e] || kk[u][e] < f.lo || kk[u][e] >= f.hi)) mismatch = 1;
       }
       if constexpr (MODE != RUN_CHECK) {
         T x[V];

@@ -3431,6 +3431,8 @@ static int run_sorted(psg_store* s, int k, const int* ops, const uint64_t* const
   }
   if (!try_same && !try_strided) return run_one_by_one(s, k, ops, keys, ns, vals, outs, st);
   RunFrames f = {};
+  f.lo = s->key_begin;
+  f.hi = s->key_end;
   for (int j = 0; j < k; ++j) {
     f.q[j] = keys[j];
     f.v[j] = (ops[j] & PSG_PUSH) ? vals[j] : nullptr;
@@ -3869,6 +3871,15 @@ int psg_store_run(psg_store* s, int k, const int* ops, const uint64_t* const* ke
   }
   if (k > 1) s->run_last = sv;
   if (served) *served = sv;
+  return PSG_OK;
+}
+
+int psg_store_set_key_range(psg_store* s, uint64_t key_begin, uint64_t key_end) {
+  PSG_REQUIRE(s && s->kind == PSG_STORE_SORTED && key_begin < key_end, PSG_ERR_INVALID,
+              "psg_store_set_key_range: a SORTED store and a non-empty range");
+  PSG_TRY(drain(s));
+  s->key_begin = key_begin;
+  s->key_end = key_end;
   return PSG_OK;
 }
 

@@ -220,13 +220,13 @@ inline void TraceRequest(int server, const KVMeta& m, size_t keys, size_t run_si
   if (len > 0) (void)!::write(fd, line, (size_t)len);
 }
 
-/* PS_SPEC_SLICE=1: a worker sends an HBM key list it sliced before on the
- * bounds it had then, unconfirmed, when every server checks its slices
- * (KVWorker::Send; default 0). */
+/* A worker sends an HBM key list it sliced before on the bounds it had then,
+ * unconfirmed, when every server checks its slices (KVWorker::Send);
+ * PS_SPEC_SLICE=0: every request is sliced first (A/B). */
 inline bool SpecSliceOn() {
   static const bool on = [] {
     const char* e = std::getenv("PS_SPEC_SLICE");
-    return e && std::atoi(e) != 0;
+    return !(e && std::atoi(e) == 0);
   }();
   return on;
 }
@@ -810,12 +810,12 @@ struct KVServerDefaultHandle {
       }
     }
     std::vector<int> status(k, PSG_OK);
+    bool any_spec = false;
+    for (const auto& it : run) any_spec = any_spec || it.spec;
     {
       stage::Scope t("server.handle.store.run");
-      int served = 0;
-      const int rc = psg_store_run_status(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(),
-                                          op.data(), s, &served, status.data());
-      if (rc != PSG_OK) device::Check(rc, "psg_store_run");
+      ServeRun(any_spec, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), op.data(), s, status.data(),
+               [&](int j) { return run[j].spec; });
     }
     // a request refused for a key outside this shard: fatal, as a CHECK,
     // unless its slice was the worker's unconfirmed hint
@@ -898,10 +898,10 @@ struct KVServerDefaultHandle {
       }
       std::vector<int> ops(k, PSG_PUSH);
       std::vector<uint64_t> ns(k, n);
-      int served = 0;
-      const int rc = psg_store_run_status(state->store, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), nullptr,
-                                          s, &served, status.data());
-      if (rc != PSG_OK) device::Check(rc, "psg_store_run");
+      bool any_spec = false;
+      for (char c : spec) any_spec = any_spec || c;
+      ServeRun(any_spec, (int)k, ops.data(), kp.data(), ns.data(), vp.data(), nullptr, s, status.data(),
+               [&](int j) { return j < (int)spec.size() && spec[j] != 0; });
       for (size_t j = 0; j < k; ++j)
         if (status[j] != PSG_OK && !(j < spec.size() && spec[j])) device::Check(status[j], "psg_store_run");
       if (state->key_cache)
@@ -913,6 +913,33 @@ struct KVServerDefaultHandle {
     for (size_t j = 0; j < metas.size(); ++j) {
       if (status[j] != PSG_OK) server->RunRefuse(metas[j]);
       else server->Response(metas[j], KVPairs<Value>());
+    }
+  }
+
+  /* A run through psg_store_run_status.  A run holding unconfirmed slices
+   * (KVRunItem::spec) is served against this server's own key range, so a
+   * slice with a key outside it is refused (nothing of it applied); a request
+   * of the run that is not such a slice and was refused only for that
+   * narrower range is then served again on the whole range. */
+  template <typename IsSpec>
+  void ServeRun(bool any_spec, int k, const int* ops, const uint64_t* const* kp, const uint64_t* ns,
+                const void* const* vp, void* const* op, psg_stream s, int* status, IsSpec is_spec) {
+    int served = 0;
+    if (!any_spec) {
+      const int rc = psg_store_run_status(state->store, k, ops, kp, ns, vp, op, s, &served, status);
+      if (rc != PSG_OK) device::Check(rc, "psg_store_run");
+      return;
+    }
+    const auto& r = PostOffice::Get()->GetServerRanges()[PostOffice::IDToRank(PostOffice::Get()->my_id())];
+    device::Check(psg_store_set_key_range(state->store, r.begin, r.end), "psg_store_set_key_range");
+    const int rc = psg_store_run_status(state->store, k, ops, kp, ns, vp, op, s, &served, status);
+    device::Check(psg_store_set_key_range(state->store, 0, kMaxKey), "psg_store_set_key_range");
+    if (rc != PSG_OK) device::Check(rc, "psg_store_run");
+    for (int j = 0; j < k; ++j) {
+      if (status[j] != PSG_ERR_RANGE || is_spec(j)) continue;
+      const int rc1 = psg_store_run_status(state->store, 1, ops + j, kp + j, ns + j, vp + j, op ? op + j : nullptr, s,
+                                           &served, status + j);
+      if (rc1 != PSG_OK) device::Check(rc1, "psg_store_run");
     }
   }
 
@@ -1266,7 +1293,7 @@ void KVWorker<Value>::Send(int timestamp, bool push, bool pull, int cmd, const D
   SlicedKVs sliced;
   const std::vector<Range>& ranges = PostOffice::Get()->GetServerRanges();
   const size_t ns = ranges.size();
-  // Unconfirmed slices (PS_SPEC_SLICE): an HBM key list this thread sliced
+  // Unconfirmed slices (PS_SPEC_SLICE=0: off): an HBM key list this thread sliced
   // before is sent on the bounds it had then, without the slicer's kernel and
   // readback, when every server's handle checks each key against its own
   // range (a wrong bound puts some key outside its server's range; that

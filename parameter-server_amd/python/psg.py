@@ -46,7 +46,7 @@ EXPORTS = [
     "psg_store_handle", "psg_store_handle_async", "psg_store_wait", "psg_sort_pairs_u64", "psg_store_resolve", "psg_store_handle_slots",
     "psg_store_slots_stretch", "psg_store_handle_stretch", "psg_store_sync", "psg_store_dump",
     "psg_key_list_hash", "psg_store_push_frames", "psg_store_push_slots_frames", "psg_store_run",
-    "psg_store_run_status", "psg_server_ranges", "psg_slice", "psg_slice_hint", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
+    "psg_store_run_status", "psg_store_set_key_range", "psg_server_ranges", "psg_slice", "psg_slice_hint", "psg_merge", "psg_comm_id_bytes", "psg_comm_get_id",
     "psg_comm_init", "psg_comm_destroy", "psg_comm_rank", "psg_comm_push", "psg_comm_pull",
     "psg_comm_push_pull", "psg_comm_push_keyed", "psg_comm_pull_keyed",
     "psg_comm_bucket_plan", "psg_comm_keyed_plan", "psg_comm_sync", "psg_comm_abort",
@@ -136,6 +136,7 @@ def lib() -> C.CDLL:
             "psg_store_run_status": ([vp, i32, C.POINTER(i32), C.POINTER(vp), C.POINTER(u64), C.POINTER(vp),
                                       C.POINTER(vp), vp, C.POINTER(i32), C.POINTER(i32)], i32),
             "psg_slice_hint": ([vp, u64, i32, u64, vp, C.POINTER(i32)], i32),
+            "psg_store_set_key_range": ([vp, u64, u64], i32),
             "psg_server_ranges": ([i32, vp, vp], i32),
             "psg_slice": ([vp, u64, vp, u64, i32, vp, vp, vp, vp, vp], i32),
             "psg_merge": ([C.POINTER(Segment), i32, i32, vp, u64, vp], i32),
