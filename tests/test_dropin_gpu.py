@@ -55,26 +55,33 @@ def test_reference_test_kv_app(ns, nw):
     _all_errors_zero(r.stdout, nw)
 
 
-@pytest.mark.parametrize("ns,nw,procs", [(2, 1, False), (4, 2, False), (8, 1, False), (2, 2, True),
-                                         (8, 2, True)])
-def test_reference_test_kv_app_on_the_device_slicer(ns, nw, procs):
+@pytest.mark.parametrize("ns,nw,procs,spec", [(2, 1, False, 0), (4, 2, False, 0), (8, 1, False, 0), (2, 2, True, 0),
+                                              (8, 2, True, 0), (4, 2, False, 1), (8, 2, True, 1)])
+def test_reference_test_kv_app_on_the_device_slicer(ns, nw, procs, spec):
     """The reference's test_kv_app.cpp with its own host vectors staged into
     HBM (PS_STAGE_MIN_BYTES=1: every array once the servers said they take HBM
     frames), so its requests are cut by the device slicer (psg_slice) into
     HBM frames and its Pull replies are merged by psg_merge — under the
     reference program's own CHECKs (test_kv_app.cpp:50-60).  The servers'
     stores reject a key outside their range (PSG_ERR_RANGE), so a slice bound
-    off by one key fails the job rather than passing unnoticed."""
+    off by one key fails the job rather than passing unnoticed.  spec = 1:
+    with unconfirmed slices (PS_SPEC_SLICE, the default), where a list sliced
+    before goes out on its last bounds and the servers' range checks confirm
+    them — the program's CHECKs still hold."""
     exe = os.path.join(DROPIN, "test_kv_app")
     _need(exe)
     args = ["-ns", ns, "-nw", nw] + (["-procs"] if procs else [])
-    r = run(exe, *args, env={"PS_STAGE_MIN_BYTES": "1", "PS_STAGE_TIMES": "1"})
+    r = run(exe, *args, env={"PS_STAGE_MIN_BYTES": "1", "PS_STAGE_TIMES": "1", "PS_SPEC_SLICE": str(spec)})
     assert r.returncode == 0, r.stderr[-3000:]
     _all_errors_zero(r.stdout, nw)
     sliced = r.stderr.count("worker.slice.device")
-    # 50 Pushes, 1 Pull and 50 PushPulls per worker; all but the first few
-    # (before the servers' hbm_handle replies arrive) go through psg_slice
-    assert sliced >= nw * 80, (sliced, r.stderr[-2000:])
+    if not spec:
+        # 50 Pushes, 1 Pull and 50 PushPulls per worker; all but the first few
+        # (before the servers' hbm_handle replies arrive) go through psg_slice
+        assert sliced >= nw * 80, (sliced, r.stderr[-2000:])
+    else:
+        # a list is sliced for real once, then sent on its bounds
+        assert sliced >= 1, r.stderr[-2000:]
 
 
 def test_reference_multi_workers():
