@@ -62,9 +62,8 @@ def test_reference_test_kv_app_on_the_device_slicer(ns, nw, procs, spec):
     HBM (PS_STAGE_MIN_BYTES=1: every array once the servers said they take HBM
     frames), so its requests are cut by the device slicer (psg_slice) into
     HBM frames and its Pull replies are merged by psg_merge — under the
-    reference program's own CHECKs (test_kv_app.cpp:50-60).  The servers'
-    stores reject a key outside their range (PSG_ERR_RANGE), so a slice bound
-    off by one key fails the job rather than passing unnoticed.  spec = 1:
+    reference program's own CHECKs (test_kv_app.cpp:50-60); the bounds
+    themselves are pinned by test_gpu_parity's KATs through psg_slice.  spec = 1:
     with unconfirmed slices (PS_SPEC_SLICE, the default), where a list sliced
     before goes out on its last bounds and the servers' range checks confirm
     them — the program's CHECKs still hold."""
